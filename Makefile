@@ -1,0 +1,87 @@
+# xrabit native build: host runtime (g++) + gfx950 HIP kernels (hipcc), linked against
+# libamdhip64 and librccl.  Outputs land in-tree (rabit_amd/lib) so they travel with the
+# repository snapshot to the GPU box.
+#
+#   make -j8            libraries (robust/base/mock/empty flavours, same names as rabit)
+#   make tests          C++ unit-test and integration programs in build/bin
+#   make clean
+
+ROCM      ?= /opt/rocm
+CXX       ?= g++
+HIPCC     ?= $(ROCM)/bin/hipcc
+ARCH      ?= gfx950
+OPT       ?= -O3
+SAN       ?=
+
+BUILD     := build
+OBJ       := $(BUILD)/obj
+LIBDIR    := rabit_amd/lib
+BIN       := $(BUILD)/bin
+
+INC       := -Icsrc/include -Icsrc/src -I$(ROCM)/include
+CXXFLAGS  := $(OPT) -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread \
+             -D__HIP_PLATFORM_AMD__ $(INC) $(SAN)
+HIPFLAGS  := $(OPT) -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(INC)
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
+
+CORE_SRCS := csrc/src/core/log.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc \
+             csrc/src/coll/host_coll.cc csrc/src/device/device_plane.cc \
+             csrc/src/engine/engine_base.cc csrc/src/engine/engine_robust.cc \
+             csrc/src/engine/recovery.cc csrc/src/capi/c_api.cc
+CORE_OBJS := $(patsubst csrc/src/%.cc,$(OBJ)/%.o,$(CORE_SRCS))
+KERN_OBJ  := $(OBJ)/device/kernels.o
+HEADERS   := $(shell find csrc -name '*.h')
+
+FLAVOURS  := rabit rabit_base rabit_mock rabit_empty
+LIBS      := $(foreach f,$(FLAVOURS),$(LIBDIR)/lib$(f).so) $(LIBDIR)/librabit_mock.a
+
+.PHONY: all libs tests clean
+all: libs
+libs: $(LIBS)
+
+$(OBJ)/%.o: csrc/src/%.cc $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(KERN_OBJ): csrc/src/device/kernels.hip csrc/src/device/kernels.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# one registry object per flavour: only the default engine differs
+$(OBJ)/registry_%.o: csrc/src/engine/registry.cc $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -DXRABIT_DEFAULT_ENGINE='"$*"' -c $< -o $@
+
+$(LIBDIR)/librabit.so: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_robust.o
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+$(LIBDIR)/librabit_base.so: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_base.o
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+$(LIBDIR)/librabit_mock.so: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_mock.o
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+$(LIBDIR)/librabit_empty.so: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_empty.o
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+$(LIBDIR)/librabit_mock.a: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_mock.o
+	@mkdir -p $(LIBDIR)
+	rm -f $@ && ar rcs $@ $^
+
+# ---------------------------------------------------------------- test / example programs
+TEST_PROGS := unit_tests model_recover local_recover lazy_recover speed_test basic \
+              broadcast lazy_allreduce device_selftest
+tests: $(foreach p,$(TEST_PROGS),$(BIN)/$(p))
+
+$(BIN)/unit_tests: tests/cpp/unit_tests.cc $(LIBDIR)/librabit_mock.a $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) $(CXXFLAGS) $< $(LIBDIR)/librabit_mock.a -o $@ $(LDLIBS)
+$(BIN)/%: tests/cpp/%.cc $(LIBDIR)/librabit_mock.so $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lrabit_mock -Wl,-rpath,$(abspath $(LIBDIR)) $(LDLIBS)
+$(BIN)/%: examples/%.cc $(LIBDIR)/librabit.so $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lrabit -Wl,-rpath,$(abspath $(LIBDIR)) $(LDLIBS)
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)/*.so $(LIBDIR)/*.a

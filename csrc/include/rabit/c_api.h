@@ -1,0 +1,98 @@
+/*!
+ * \file c_api.h
+ * \brief C API of xrabit, ABI compatible with the reference (`include/rabit/c_api.h:24-194`)
+ *        plus device extensions (RabitDev..., RabitSet... functions).
+ *
+ * Pointers handed to RabitAllreduce/RabitBroadcast/RabitAllgather may be host memory or
+ * HBM; the engine detects which.
+ */
+#ifndef RABIT_C_API_H_
+#define RABIT_C_API_H_
+
+#ifdef __cplusplus
+#define RABIT_EXTERN_C extern "C"
+#include <cstddef>
+#include <cstdint>
+#else
+#define RABIT_EXTERN_C
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+#endif
+
+#define RABIT_DLL RABIT_EXTERN_C __attribute__((visibility("default")))
+
+/*! \brief unsigned long, kept for ABI compatibility */
+typedef unsigned long rbt_ulong;  // NOLINT(*)
+
+RABIT_DLL bool RabitInit(int argc, char *argv[]);
+RABIT_DLL bool RabitFinalize(void);
+RABIT_DLL int RabitGetRingPrevRank(void);
+RABIT_DLL int RabitGetRank(void);
+RABIT_DLL int RabitGetWorldSize(void);
+RABIT_DLL int RabitIsDistributed(void);
+RABIT_DLL void RabitTrackerPrint(const char *msg);
+RABIT_DLL void RabitGetProcessorName(char *out_name, rbt_ulong *out_len, rbt_ulong max_len);
+RABIT_DLL void RabitBroadcast(void *sendrecv_data, rbt_ulong size, int root);
+/*! \brief allgather; indices are in elements of enum_dtype */
+RABIT_DLL void RabitAllgather(void *sendrecvbuf, size_t total_size, size_t beginIndex,
+                              size_t size_node_slice, size_t size_prev_slice, int enum_dtype);
+RABIT_DLL void RabitAllreduce(void *sendrecvbuf, size_t count, int enum_dtype, int enum_op,
+                              void (*prepare_fun)(void *arg), void *prepare_arg);
+/*!
+ * \brief load the latest checkpoint; the returned pointers stay valid until the next call
+ *        from the same thread.  out_local_model may be NULL.
+ */
+RABIT_DLL int RabitLoadCheckPoint(char **out_global_model, rbt_ulong *out_global_len,
+                                  char **out_local_model, rbt_ulong *out_local_len);
+RABIT_DLL void RabitCheckPoint(const char *global_model, rbt_ulong global_len,
+                               const char *local_model, rbt_ulong local_len);
+/*! \brief lazy checkpoint of a global blob: only the pointer is kept, the caller must keep
+ *         the blob alive and unchanged until the next checkpoint (xrabit extension) */
+RABIT_DLL void RabitLazyCheckPoint(const char *global_model, rbt_ulong global_len);
+RABIT_DLL int RabitVersionNumber(void);
+/*! \brief a dummy function used to verify the library was linked */
+RABIT_DLL int RabitLinkTag(void);
+
+// ---------------- xrabit extensions ----------------
+/*! \brief name of the active engine ("robust", "base", "mock", "empty") */
+RABIT_DLL const char *RabitEngineName(void);
+/*! \brief order device collectives after the given hipStream_t (NULL = null stream) */
+RABIT_DLL void RabitSetStream(void *hip_stream);
+/*! \brief device ordinal of the engine, -1 if none */
+RABIT_DLL int RabitGetDevice(void);
+/*! \brief 1 if ptr is device memory */
+RABIT_DLL int RabitIsDevicePointer(const void *ptr);
+/*!
+ * \brief fused "lazy prepare" allreduce for HBM buffers: dst = prep(src) then allreduce(dst).
+ *        prep_op: 0 copy, 1 square (g*g), 2 scale by alpha, 3 abs.  The prepare kernel is
+ *        skipped when the result is recovered from peers (rabit lazy-prepare semantics).
+ */
+RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t count,
+                                         int enum_dtype, int enum_op, int prep_op,
+                                         double alpha);
+/*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
+ *         1: an error is recorded (RabitGetLastError) and the call returns */
+RABIT_DLL void RabitSetErrorMode(int mode);
+/*! \brief last error message of this thread (empty if none) */
+RABIT_DLL const char *RabitGetLastError(void);
+/*! \brief engine statistics as a JSON string (recoveries, bytes, per-op timing) */
+RABIT_DLL const char *RabitGetStats(void);
+
+// ---------------- device kernel entry points (tests / python ops) ----------------
+/*! \brief dst[i] = op(dst[i], src[i]) on device buffers, enqueued on stream */
+RABIT_DLL int RabitDevReduce(void *dst, const void *src, size_t count, int enum_dtype,
+                             int enum_op, void *hip_stream);
+/*! \brief dst[i] = op(srcs[0][i], ..., srcs[nsrc-1][i]) (nsrc <= 8) */
+RABIT_DLL int RabitDevReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
+                                  int enum_dtype, int enum_op, void *hip_stream);
+/*! \brief dst = prep(src) and, if dst2 != NULL, dst2 = prep(src) in the same pass */
+RABIT_DLL int RabitDevPrepare(void *dst, void *dst2, const void *src, size_t count,
+                              int enum_dtype, int prep_op, double alpha, void *hip_stream);
+/*! \brief 64-bit position-weighted checksum of nbytes (nbytes % 4 == 0) into *out (device u64) */
+RABIT_DLL int RabitDevChecksum(const void *buf, size_t nbytes, void *out_dev_u64,
+                               void *hip_stream);
+/*! \brief fill count elements with value */
+RABIT_DLL int RabitDevFill(void *dst, size_t count, int enum_dtype, double value,
+                           void *hip_stream);
+#endif  // RABIT_C_API_H_

@@ -1,0 +1,392 @@
+/*!
+ * \file device_plane.cc
+ * \brief RCCL + HIP implementation of the device data plane.
+ */
+#include "device/device_plane.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "device/kernels.h"
+#include "rabit/internal/utils.h"
+
+namespace rabit {
+namespace device {
+
+void CheckHip(hipError_t e, const char *what) {
+  if (e != hipSuccess) utils::Error("HIP error in %s: %s", what, hipGetErrorString(e));
+}
+
+namespace {
+void CheckNccl(ncclResult_t r, const char *what) {
+  if (r != ncclSuccess) utils::Error("RCCL error in %s: %s", what, ncclGetErrorString(r));
+}
+
+bool RcclType(int dtype, ncclDataType_t *out) {
+  switch (dtype) {
+    case 0: *out = ncclInt8; return true;
+    case 1: *out = ncclUint8; return true;
+    case 2: *out = ncclInt32; return true;
+    case 3: *out = ncclUint32; return true;
+    case 4: *out = ncclInt64; return true;
+    case 5: *out = ncclUint64; return true;
+    case 6: *out = ncclFloat32; return true;
+    case 7: *out = ncclFloat64; return true;
+    case 8: *out = ncclInt64; return true;
+    case 9: *out = ncclUint64; return true;
+    default: return false;
+  }
+}
+
+bool RcclOp(int op, ncclRedOp_t *out) {
+  switch (op) {
+    case 0: *out = ncclMax; return true;
+    case 1: *out = ncclMin; return true;
+    case 2: *out = ncclSum; return true;
+    default: return false;  // BitOR: no RCCL equivalent
+  }
+}
+
+size_t TypeBytes(int dtype) {
+  switch (dtype) {
+    case 0:
+    case 1: return 1;
+    case 2:
+    case 3:
+    case 6: return 4;
+    default: return 8;
+  }
+}
+}  // namespace
+
+// ------------------------------------------------------------------ arena
+DeviceArena::~DeviceArena() {
+  for (auto &c : chunks_) (void)hipFree(c.base);
+}
+
+void *DeviceArena::Alloc(size_t bytes) {
+  const size_t need = (bytes + 255) & ~static_cast<size_t>(255);
+  while (cur_ < chunks_.size()) {
+    Chunk &c = chunks_[cur_];
+    if (c.size - c.used >= need) {
+      void *p = c.base + c.used;
+      c.used += need;
+      return p;
+    }
+    if (cur_ + 1 == chunks_.size()) break;
+    ++cur_;
+  }
+  if (reserved() + std::max(need, chunk_) > cap_) return nullptr;
+  Chunk c;
+  c.size = std::max(need, chunk_);
+  c.used = need;
+  void *base = nullptr;
+  if (hipMalloc(&base, c.size) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  c.base = static_cast<char *>(base);
+  chunks_.push_back(c);
+  cur_ = chunks_.size() - 1;
+  return c.base;
+}
+
+void DeviceArena::PopTo(void *ptr) {
+  char *p = static_cast<char *>(ptr);
+  for (size_t i = 0; i < chunks_.size(); ++i) {
+    Chunk &c = chunks_[i];
+    if (p >= c.base && p < c.base + c.size) {
+      c.used = static_cast<size_t>(p - c.base);
+      for (size_t j = i + 1; j < chunks_.size(); ++j) chunks_[j].used = 0;
+      cur_ = i;
+      return;
+    }
+  }
+}
+
+void DeviceArena::Reset() {
+  for (auto &c : chunks_) c.used = 0;
+  cur_ = 0;
+}
+
+size_t DeviceArena::used() const {
+  size_t s = 0;
+  for (auto &c : chunks_) s += c.used;
+  return s;
+}
+
+size_t DeviceArena::reserved() const {
+  size_t s = 0;
+  for (auto &c : chunks_) s += c.size;
+  return s;
+}
+
+// ------------------------------------------------------------------ plane
+int DevicePlane::DeviceCount() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
+  const int ndev = DeviceCount();
+  utils::Check(ndev > 0, "DevicePlane: no HIP device visible");
+  int dev = cfg.device;
+  if (dev < 0) {
+    const char *lr = getenv("LOCAL_RANK");
+    dev = lr != nullptr ? atoi(lr) : std::max(rank_hint, 0);
+  }
+  device_ = dev % ndev;
+  CheckHip(hipSetDevice(device_), "hipSetDevice");
+  CheckHip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  CheckHip(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
+  CheckHip(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
+  arena_.Configure(cfg.arena_chunk, cfg.arena_cap);
+}
+
+DevicePlane::~DevicePlane() {
+  if (stream_ != nullptr) (void)hipStreamSynchronize(stream_);
+  if (comm_ != nullptr) {
+    ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (scratch_[i] != nullptr) (void)hipFree(scratch_[i]);
+  }
+  if (pinned_ != nullptr) (void)hipHostFree(pinned_);
+  if (ev_in_ != nullptr) (void)hipEventDestroy(ev_in_);
+  if (ev_done_ != nullptr) (void)hipEventDestroy(ev_done_);
+  if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
+}
+
+bool DevicePlane::IsDevicePtr(const void *p) const {
+  if (p == nullptr) return false;
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+std::string DevicePlane::NewUniqueId() {
+  ncclUniqueId id;
+  CheckNccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
+                             const FailureProbe &probe) {
+  (void)probe;
+  if (comm_ != nullptr) AbortComm();
+  utils::Check(id_bytes.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
+  ncclUniqueId id;
+  std::memcpy(id.internal, id_bytes.data(), sizeof(id.internal));
+  CheckHip(hipSetDevice(device_), "hipSetDevice");
+  ncclResult_t r = ncclCommInitRank(&comm_, nranks, id, rank);
+  if (r != ncclSuccess) {
+    comm_ = nullptr;
+    utils::HandleLogInfo("[xrabit] ncclCommInitRank failed: %s\n", ncclGetErrorString(r));
+    return Status::kAborted;
+  }
+  nranks_ = nranks;
+  rank_ = rank;
+  ++epoch_;
+  return Status::kSuccess;
+}
+
+void DevicePlane::AbortComm() {
+  if (comm_ != nullptr) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
+void DevicePlane::EnterFromUser() {
+  if (user_stream_ == stream_) return;
+  CheckHip(hipEventRecord(ev_in_, user_stream_), "hipEventRecord(user)");
+  CheckHip(hipStreamWaitEvent(stream_, ev_in_, 0), "hipStreamWaitEvent");
+}
+
+Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  for (uint64_t iter = 0;; ++iter) {
+    hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return Status::kSuccess;
+    if (e != hipErrorNotReady) CheckHip(e, "device collective");
+    if (comm_ != nullptr && (iter & 15) == 0) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess &&
+          ae != ncclInProgress) {
+        utils::HandleLogInfo("[xrabit] RCCL async error: %s\n", ncclGetErrorString(ae));
+        AbortComm();
+        return Status::kAborted;
+      }
+    }
+    const double waited = std::chrono::duration<double>(clock::now() - t0).count();
+    if (probe && (iter & 63) == 0 && waited > 1e-3 && probe()) {
+      AbortComm();
+      (void)hipStreamSynchronize(stream_);
+      return Status::kAborted;
+    }
+    if (cfg_.op_timeout_sec > 0 && waited > cfg_.op_timeout_sec) {
+      utils::HandleLogInfo("[xrabit] device op exceeded %.1f s, aborting communicator\n",
+                           cfg_.op_timeout_sec);
+      AbortComm();
+      (void)hipStreamSynchronize(stream_);
+      return Status::kTimeout;
+    }
+    if (waited * 1e6 > cfg_.spin_us) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
+  CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
+  if (user_stream_ != stream_) {
+    CheckHip(hipStreamWaitEvent(user_stream_, ev_done_, 0), "hipStreamWaitEvent(user)");
+  }
+  if (!cfg_.sync || !host_wait) return Status::kSuccess;
+  return WaitEvent(ev_done_, probe);
+}
+
+void DevicePlane::Synchronize() { CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
+
+void DevicePlane::CopyAsync(void *dst, const void *src, size_t bytes) {
+  if (bytes == 0 || dst == src) return;
+  CheckHip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+}
+
+void *DevicePlane::Scratch(size_t bytes, int slot) {
+  if (scratch_bytes_[slot] < bytes) {
+    if (scratch_[slot] != nullptr) {
+      CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+      (void)hipFree(scratch_[slot]);
+    }
+    size_t want = std::max(bytes, scratch_bytes_[slot] * 2);
+    CheckHip(hipMalloc(&scratch_[slot], want), "hipMalloc(scratch)");
+    scratch_bytes_[slot] = want;
+  }
+  return scratch_[slot];
+}
+
+void DevicePlane::StageToHost(void *host, const void *dev, size_t bytes) {
+  CheckHip(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
+  CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+void DevicePlane::StageToDevice(void *dev, const void *host, size_t bytes) {
+  CheckHip(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream_), "H2D");
+  CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+Status DevicePlane::Allreduce(const void *send, void *recv, size_t count, int dtype, int op,
+                              const FailureProbe &probe) {
+  utils::Check(comm_ != nullptr, "device allreduce without communicator");
+  ncclDataType_t t;
+  ncclRedOp_t o;
+  if (!RcclType(dtype, &t)) utils::Error("unsupported dtype %d on device", dtype);
+  if (!RcclOp(op, &o)) return AllreduceByKernel(send, recv, count, dtype, op, probe);
+  CheckNccl(ncclAllReduce(send, recv, count, t, o, comm_, stream_), "ncclAllReduce");
+  return Status::kSuccess;
+}
+
+Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count, int dtype,
+                                      int op, const FailureProbe &probe) {
+  (void)probe;
+  const size_t tn = TypeBytes(dtype);
+  const int n = nranks_;
+  if (n == 1) {
+    CopyAsync(recv, send, count * tn);
+    return Status::kSuccess;
+  }
+  // all-to-all: rank k receives everyone's copy of segment k, reduces it with the
+  // multi-source kernel, then an allgather distributes the reduced segments
+  const size_t seg = (count + n - 1) / n;
+  const size_t seg_bytes = ((seg * tn + 255) / 256) * 256;  // keep segments 256-B aligned
+  char *a = static_cast<char *>(Scratch(seg_bytes * n, 0));
+  char *b = static_cast<char *>(Scratch(seg_bytes * n, 1));
+  // pack the input as n segments of seg_bytes
+  for (int k = 0; k < n; ++k) {
+    const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
+    if (hi > lo) {
+      CheckHip(hipMemcpyAsync(a + k * seg_bytes, static_cast<const char *>(send) + lo * tn,
+                              (hi - lo) * tn, hipMemcpyDeviceToDevice, stream_),
+               "pack");
+    }
+  }
+  CheckNccl(ncclAllToAll(a, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllToAll");
+  // reduce the n copies of my segment, 8 sources per kernel pass
+  char *mine = a + static_cast<size_t>(rank_) * seg_bytes;
+  std::vector<const void *> srcs;
+  int done = 0;
+  while (done < n) {
+    srcs.clear();
+    if (done > 0) srcs.push_back(mine);
+    while (done < n && static_cast<int>(srcs.size()) < kMaxReduceSources) {
+      srcs.push_back(b + static_cast<size_t>(done) * seg_bytes);
+      ++done;
+    }
+    CheckHip(LaunchReduceMulti(mine, srcs.data(), static_cast<int>(srcs.size()), seg, dtype, op,
+                               stream_),
+             "LaunchReduceMulti");
+  }
+  CheckNccl(ncclAllGather(mine, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+  for (int k = 0; k < n; ++k) {
+    const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
+    if (hi > lo) {
+      CheckHip(hipMemcpyAsync(static_cast<char *>(recv) + lo * tn, b + k * seg_bytes,
+                              (hi - lo) * tn, hipMemcpyDeviceToDevice, stream_),
+               "unpack");
+    }
+  }
+  return Status::kSuccess;
+}
+
+Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe) {
+  (void)probe;
+  utils::Check(comm_ != nullptr, "device broadcast without communicator");
+  CheckNccl(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
+  return Status::kSuccess;
+}
+
+Status DevicePlane::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
+                               const std::vector<size_t> &size, const FailureProbe &probe) {
+  (void)probe;
+  utils::Check(comm_ != nullptr, "device allgather without communicator");
+  char *buf = static_cast<char *>(buf_);
+  const int n = nranks_;
+  bool uniform = total == size[0] * n;
+  for (int r = 0; r < n && uniform; ++r) uniform = begin[r] == r * size[0] && size[r] == size[0];
+  if (uniform) {
+    CheckNccl(ncclAllGather(buf + begin[rank_], buf, size[0], ncclUint8, comm_, stream_),
+              "ncclAllGather");
+    return Status::kSuccess;
+  }
+  CheckNccl(ncclGroupStart(), "ncclGroupStart");
+  for (int r = 0; r < n; ++r) {
+    size_t b = begin[r] % total, s = size[r];
+    const size_t first = std::min(s, total - b);
+    if (first != 0) {
+      CheckNccl(ncclBroadcast(buf + b, buf + b, first, ncclUint8, r, comm_, stream_),
+                "ncclBroadcast");
+    }
+    if (s > first) {
+      CheckNccl(ncclBroadcast(buf, buf, s - first, ncclUint8, r, comm_, stream_),
+                "ncclBroadcast");
+    }
+  }
+  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+  return Status::kSuccess;
+}
+}  // namespace device
+}  // namespace rabit

@@ -1,0 +1,144 @@
+/*!
+ * \file device_plane.h
+ * \brief Device data plane: RCCL over xGMI + gfx950 kernels for HBM buffers.
+ *
+ * MI355X design:
+ *  - one process per GPU, one RCCL communicator per engine; the ncclUniqueId travels over the
+ *    host control plane (the engine broadcasts it on the TCP tree), and a new communicator
+ *    (new epoch) is built after every recovery;
+ *  - built-in Sum/Max/Min go to ncclAllReduce; ops RCCL lacks (BitOR) use
+ *    all-to-all + our multi-source reduce kernel + allgather (bandwidth-optimal, all 7 links);
+ *  - rabit's variable, wrapping Allgather slices become a group of ncclBroadcast calls;
+ *  - collectives run on a private non-blocking stream ordered after the caller's stream by
+ *    events; the host waits on completion while probing for peer failure (TCP hang-up) and
+ *    RCCL async errors, and aborts the communicator (ncclCommAbort) so a dead peer can never
+ *    wedge the process.
+ */
+#ifndef XRABIT_DEVICE_DEVICE_PLANE_H_
+#define XRABIT_DEVICE_DEVICE_PLANE_H_
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "net/socket.h"
+
+namespace rabit {
+namespace device {
+
+using net::Status;
+
+/*! \brief returns true when a peer failure was detected (checked while waiting) */
+typedef std::function<bool()> FailureProbe;
+
+struct DeviceConfig {
+  int device{-1};                      // -1: LOCAL_RANK env, else rank % device count
+  bool sync{true};                     // host waits for each collective to complete
+  double op_timeout_sec{0};            // 0: no deadline on a device op
+  size_t arena_chunk{256u << 20};      // result-log arena growth step
+  size_t arena_cap{size_t(64) << 30};  // beyond this the result log falls back to host memory
+  int spin_us{50};                     // busy-poll window before sleeping while waiting
+};
+
+/*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
+ *  chunks; Reset() keeps the chunks so steady-state iterations never call hipMalloc) */
+class DeviceArena {
+ public:
+  ~DeviceArena();
+  void Configure(size_t chunk, size_t cap) {
+    chunk_ = chunk;
+    cap_ = cap;
+  }
+  /*! \brief 256-byte aligned slot, nullptr when over the cap or out of memory */
+  void *Alloc(size_t bytes);
+  /*! \brief give back the most recent allocation (ResultLog::DropLast) */
+  void PopTo(void *ptr);
+  void Reset();
+  size_t used() const;
+  size_t reserved() const;
+
+ private:
+  struct Chunk {
+    char *base;
+    size_t size, used;
+  };
+  std::vector<Chunk> chunks_;
+  size_t cur_{0};
+  size_t chunk_{256u << 20}, cap_{size_t(64) << 30};
+};
+
+class DevicePlane {
+ public:
+  /*! \brief number of visible GPUs (0 when HIP has no device) */
+  static int DeviceCount();
+  DevicePlane(const DeviceConfig &cfg, int rank_hint);
+  ~DevicePlane();
+
+  int device() const { return device_; }
+  bool IsDevicePtr(const void *p) const;
+  void SetUserStream(hipStream_t s) { user_stream_ = s; }
+  hipStream_t stream() const { return stream_; }
+  DeviceArena *arena() { return &arena_; }
+  const DeviceConfig &config() const { return cfg_; }
+
+  // ---- communicator lifecycle
+  /*! \brief serialized ncclUniqueId (NCCL_UNIQUE_ID_BYTES bytes) */
+  static std::string NewUniqueId();
+  /*! \brief collective over all ranks: build the communicator of a new epoch */
+  Status InitComm(const std::string &id, int nranks, int rank, const FailureProbe &probe);
+  /*! \brief abort the communicator (unblocks in-flight kernels), drop it */
+  void AbortComm();
+  bool has_comm() const { return comm_ != nullptr; }
+  int epoch() const { return epoch_; }
+
+  // ---- collectives (enqueue then wait)
+  /*! \brief recv = reduce(send) over ranks; send may equal recv */
+  Status Allreduce(const void *send, void *recv, size_t count, int dtype, int op,
+                   const FailureProbe &probe);
+  Status Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe);
+  /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place */
+  Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
+                    const std::vector<size_t> &size, const FailureProbe &probe);
+  /*! \brief stage a host-reducer allreduce through pinned host memory */
+  void StageToHost(void *host, const void *dev, size_t bytes);
+  void StageToDevice(void *dev, const void *host, size_t bytes);
+
+  // ---- memory / ordering
+  /*! \brief async copy on the plane stream */
+  void CopyAsync(void *dst, const void *src, size_t bytes);
+  /*! \brief order the plane stream after the user stream */
+  void EnterFromUser();
+  /*! \brief record completion, order the user stream after it, host-wait if sync */
+  Status Finish(const FailureProbe &probe, bool host_wait = true);
+  /*! \brief block until the plane stream is idle */
+  void Synchronize();
+  /*! \brief reusable scratch buffer of at least bytes */
+  void *Scratch(size_t bytes, int slot = 0);
+
+ private:
+  Status WaitEvent(hipEvent_t ev, const FailureProbe &probe);
+  Status AllreduceByKernel(const void *send, void *recv, size_t count, int dtype, int op,
+                           const FailureProbe &probe);
+
+  DeviceConfig cfg_;
+  int device_{-1};
+  hipStream_t stream_{nullptr};
+  hipStream_t user_stream_{nullptr};
+  hipEvent_t ev_in_{nullptr}, ev_done_{nullptr};
+  ncclComm_t comm_{nullptr};
+  int nranks_{0}, rank_{0}, epoch_{0};
+  DeviceArena arena_;
+  void *scratch_[2]{nullptr, nullptr};
+  size_t scratch_bytes_[2]{0, 0};
+  void *pinned_{nullptr};
+  size_t pinned_bytes_{0};
+};
+
+/*! \brief throw rabit::Error on a HIP failure */
+void CheckHip(hipError_t e, const char *what);
+}  // namespace device
+}  // namespace rabit
+#endif  // XRABIT_DEVICE_DEVICE_PLANE_H_

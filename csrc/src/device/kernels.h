@@ -1,0 +1,45 @@
+/*!
+ * \file kernels.h
+ * \brief Host-side launchers of the gfx950 HIP kernels of the device data plane.
+ *
+ * Kernel inventory: K1-K4 element-wise reduce (max/min/sum/bitor, 10
+ * dtypes), multi-source reduce (the local step of the all-to-all based allreduce used for
+ * ops RCCL lacks, e.g. BitOR), K8 fused lazy-prepare (g*g etc., optionally dual-store),
+ * and a position-weighted checksum used to validate recovered buffers and checkpoints.
+ * dtype codes are rabit::engine::mpi::DataType; op codes are mpi::OpType.
+ */
+#ifndef XRABIT_DEVICE_KERNELS_H_
+#define XRABIT_DEVICE_KERNELS_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace rabit {
+namespace device {
+
+/*! \brief prepare ops of the fused lazy-prepare kernel */
+enum PrepOp : int { kPrepCopy = 0, kPrepSquare = 1, kPrepScale = 2, kPrepAbs = 3 };
+constexpr int kMaxReduceSources = 8;
+
+/*! \brief dst[i] = op(dst[i], src[i]) */
+hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int op,
+                        hipStream_t stream);
+/*! \brief dst[i] = op(srcs[0][i], ..., srcs[nsrc-1][i]), 1 <= nsrc <= 8 (dst may alias srcs[0]) */
+hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
+                             int dtype, int op, hipStream_t stream);
+/*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
+hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
+                         int prep, double alpha, hipStream_t stream);
+/*!
+ * \brief out[0] += sum_i w_i, out[1] += sum_i (i+1) * w_i over 32-bit words (mod 2^64);
+ *        nbytes must be a multiple of 4; out must be zeroed by the caller
+ */
+hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *out,
+                          hipStream_t stream);
+/*! \brief fill count elements with value (bit pattern of dtype) */
+hipError_t LaunchFill(void *dst, size_t count, int dtype, double value, hipStream_t stream);
+}  // namespace device
+}  // namespace rabit
+#endif  // XRABIT_DEVICE_KERNELS_H_

@@ -1,0 +1,390 @@
+/*!
+ * \file engine_base.cc
+ * \brief Non-fault-tolerant engine (see engine_base.h).
+ */
+#include "engine/engine_base.h"
+
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+#include "core/params.h"
+#include "device/kernels.h"
+#include "rabit/internal/timer.h"
+#include "rabit/internal/utils.h"
+
+extern char **environ;
+
+namespace rabit {
+namespace engine {
+
+EngineBase::EngineBase() {
+  env_vars_ = {"DMLC_TASK_ID",      "DMLC_ROLE",         "DMLC_NUM_ATTEMPT",
+               "DMLC_TRACKER_URI",  "DMLC_TRACKER_PORT", "DMLC_WORKER_CONNECT_RETRY"};
+  tracker_.tcp_nodelay = true;  // the control plane is latency bound (consensus per op)
+  host_.reset(new coll::HostCollectives(&topo_, &hcfg_, &rank_, &world_size_));
+  host_->SetAbortFlag(&abort_flag_);
+}
+
+EngineBase::~EngineBase() = default;
+
+void EngineBase::SetParam(const char *name, const char *val) {
+  auto is = [name](const char *k) { return strcmp(name, k) == 0; };
+  if (is("rabit_tracker_uri") || is("DMLC_TRACKER_URI")) tracker_.uri = val;
+  if (is("rabit_tracker_port") || is("DMLC_TRACKER_PORT")) tracker_.port = atoi(val);
+  if (is("rabit_task_id") || is("DMLC_TASK_ID")) tracker_.task_id = val;
+  if (is("DMLC_ROLE")) dmlc_role_ = val;
+  if (is("rabit_world_size")) world_size_ = atoi(val);
+  if (is("rabit_hadoop_mode")) hadoop_mode_ = utils::StringToBool(val);
+  if (is("rabit_tree_reduce_minsize")) hcfg_.tree_reduce_minsize = core::ParseUnit(name, val);
+  if (is("rabit_reduce_ring_mincount")) {
+    long v = atol(val);  // NOLINT(*)
+    utils::Check(v > 0, "rabit_reduce_ring_mincount should be greater than 0");
+    hcfg_.reduce_ring_mincount = static_cast<size_t>(v);
+  }
+  if (is("rabit_reduce_buffer")) {
+    hcfg_.reduce_buffer_bytes = std::max<size_t>(core::ParseUnit(name, val), 8);
+  }
+  if (is("DMLC_WORKER_CONNECT_RETRY")) tracker_.connect_retry = atoi(val);
+  if (is("rabit_bootstrap_cache")) bootstrap_cache_ = utils::StringToBool(val);
+  if (is("rabit_debug")) debug_ = utils::StringToBool(val);
+  if (is("rabit_timeout")) timeout_enabled_ = utils::StringToBool(val);
+  if (is("rabit_timeout_sec")) {
+    timeout_sec_ = atoi(val);
+    utils::Check(timeout_sec_ >= 0, "rabit_timeout_sec should be non negative second");
+  }
+  if (is("rabit_enable_tcp_no_delay")) tracker_.tcp_nodelay = utils::StringToBool(val);
+  if (is("rabit_slave_port") || is("rabit_worker_port")) tracker_.worker_port = atoi(val);
+  if (is("rabit_nport_trial")) tracker_.nport_trial = atoi(val);
+  // ---- xrabit extensions
+  if (is("rabit_device")) dcfg_.device = atoi(val);
+  if (is("rabit_device_plane")) device_plane_mode_ = utils::StringToBool(val) ? 1 : 0;
+  if (is("rabit_device_sync")) dcfg_.sync = utils::StringToBool(val);
+  if (is("rabit_device_timeout_sec")) dcfg_.op_timeout_sec = atof(val);
+  if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
+  if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
+  if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
+  if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
+}
+
+bool EngineBase::Init(int argc, char *argv[]) {
+  // every rabit_* environment variable is a parameter too (the reference only reads a fixed
+  // list, which is kept: DMLC_* names above)
+  std::vector<std::string> names = env_vars_;
+  for (char **e = environ; e != nullptr && *e != nullptr; ++e) {
+    const char *eq = strchr(*e, '=');
+    if (eq != nullptr && strncmp(*e, "rabit_", 6) == 0) names.emplace_back(*e, eq - *e);
+  }
+  for (const auto &kv : core::CollectParams(argc, argv, names)) {
+    this->SetParam(kv.first.c_str(), kv.second.c_str());
+  }
+  // Hadoop / YARN streaming environment
+  const char *task_id = getenv("mapred_tip_id");
+  if (task_id == nullptr) task_id = getenv("mapreduce_task_id");
+  if (hadoop_mode_) utils::Check(task_id != nullptr, "hadoop_mode is set but no task id found");
+  if (task_id != nullptr) {
+    this->SetParam("rabit_task_id", task_id);
+    this->SetParam("rabit_hadoop_mode", "1");
+  }
+  const char *attempt_id = getenv("mapred_task_id");
+  if (attempt_id != nullptr) {
+    const char *att = strrchr(attempt_id, '_');
+    int trial;
+    if (att != nullptr && sscanf(att + 1, "%d", &trial) == 1) {
+      this->SetParam("rabit_num_trial", att + 1);
+    }
+  }
+  const char *num_task = getenv("mapred_map_tasks");
+  if (num_task == nullptr) num_task = getenv("mapreduce_job_maps");
+  if (hadoop_mode_) utils::Check(num_task != nullptr, "hadoop_mode is set but no task count");
+  if (num_task != nullptr) this->SetParam("rabit_world_size", num_task);
+
+  if (dmlc_role_ != "worker") {
+    fprintf(stderr, "xrabit only runs as a dmlc worker (DMLC_ROLE=%s), exiting\n",
+            dmlc_role_.c_str());
+    exit(0);
+  }
+  utils::Check(topo_.links.empty(), "can only call Init once");
+  rank_ = -1;
+  host_uri_ = net::HostName();
+  if (!ReconnectLinks("start")) return false;
+  if (device_plane_mode_ != 0 && device::DevicePlane::DeviceCount() > 0) {
+    dev_.reset(new device::DevicePlane(dcfg_, rank_));
+    if (user_stream_ != nullptr) dev_->SetUserStream(static_cast<hipStream_t>(user_stream_));
+  }
+  return true;
+}
+
+bool EngineBase::Shutdown() {
+  try {
+    if (dev_) {
+      dev_->Synchronize();
+      dev_.reset();
+    }
+    topo_.CloseAll();
+    topo_.links.clear();
+    topo_.tree.clear();
+    topo_.ring_prev = topo_.ring_next = nullptr;
+    if (tracker_.uri == "NULL") return true;
+    net::TrackerClient(&tracker_).Shutdown(rank_, world_size_);
+    return true;
+  } catch (const std::exception &e) {
+    fprintf(stderr, "xrabit: shutdown failed: %s\n", e.what());
+    return false;
+  }
+}
+
+bool EngineBase::ReconnectLinks(const char *cmd) {
+  if (tracker_.uri == "NULL") {
+    rank_ = 0;
+    world_size_ = 1;
+    return true;
+  }
+  try {
+    net::TrackerClient(&tracker_).Relink(cmd, &rank_, &world_size_, &topo_);
+    if (debug_) {
+      utils::HandleLogInfo("[%d] %s: links ready (world %d, tree %zu, ring %d<-%d->%d)\n", rank_,
+                           cmd, world_size_, topo_.tree.size(),
+                           topo_.ring_prev ? topo_.ring_prev->rank : -1, rank_,
+                           topo_.ring_next ? topo_.ring_next->rank : -1);
+    }
+    return true;
+  } catch (const std::exception &e) {
+    fprintf(stderr, "xrabit: ReconnectLinks(%s) failed: %s\n", cmd, e.what());
+    return false;
+  }
+}
+
+int EngineBase::GetRingPrevRank() const {
+  return topo_.ring_prev != nullptr ? topo_.ring_prev->rank : -1;
+}
+
+void EngineBase::TrackerPrint(const std::string &msg) {
+  if (tracker_.uri == "NULL") {
+    utils::Printf("%s", msg.c_str());
+    return;
+  }
+  net::TrackerClient(&tracker_).Print(rank_, world_size_, msg);
+}
+
+void EngineBase::SetStream(void *stream) {
+  user_stream_ = stream;
+  if (dev_) dev_->SetUserStream(static_cast<hipStream_t>(stream));
+}
+
+bool EngineBase::OnDevice(const void *p) const { return dev_ && dev_->IsDevicePtr(p); }
+
+bool EngineBase::PeerFailureProbe() const {
+  for (const auto &l : topo_.links) {
+    if (!l->sock.IsClosed() && l->sock.PeerHungUp()) return true;
+  }
+  return false;
+}
+
+void EngineBase::ReportStatus() const {
+  if (hadoop_mode_) {
+    fprintf(stderr, "reporter:status:Rabit Phase[%03d] Operation %03d\n", version_number_,
+            seq_counter_);
+  }
+}
+
+Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
+  ReduceFn red = spec.host_red;
+  if (spec.builtin()) {
+    ReduceFn fast = coll::HostReducer(static_cast<mpi::DataType>(spec.dtype),
+                                      static_cast<mpi::OpType>(spec.op));
+    if (fast != nullptr) red = fast;
+  }
+  utils::Check(red != nullptr, "Allreduce: no reducer for dtype %d op %d", spec.dtype, spec.op);
+  return host_->Allreduce(buf, spec.type_nbytes, spec.count, red);
+}
+
+Status EngineBase::EnsureDeviceComm() {
+  utils::Check(dev_ != nullptr, "device buffer given but the device plane is disabled");
+  if (dev_->has_comm()) return Status::kSuccess;
+  std::string id(sizeof(ncclUniqueId), '\0');
+  if (rank_ == 0) id = device::DevicePlane::NewUniqueId();
+  Status s = host_->TreeBroadcast(&id[0], id.size(), 0);
+  if (s != Status::kSuccess) return s;
+  return dev_->InitComm(id, GetWorldSize(), rank_, MakeProbe());
+}
+
+Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec) {
+  const size_t bytes = spec.bytes();
+  if (bytes == 0) return Status::kSuccess;
+  bool rccl_ok = spec.builtin() && spec.dtype <= mpi::kULongLong;
+  if (spec.builtin() && spec.op == mpi::kBitwiseOR &&
+      (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble)) {
+    utils::Error("BitOR is not defined for floating point types");
+  }
+  dev_->EnterFromUser();
+  if (!rccl_ok) {
+    // user-defined reducer (host function): stage through host memory
+    std::vector<uint64_t> tmp((bytes + 7) / 8);
+    dev_->StageToHost(tmp.data(), src, bytes);
+    Status s = TryAllreduceHost(tmp.data(), spec);
+    if (s != Status::kSuccess) return s;
+    dev_->StageToDevice(dst, tmp.data(), bytes);
+    return dev_->Finish(MakeProbe());
+  }
+  Status s = EnsureDeviceComm();
+  if (s != Status::kSuccess) return s;
+  stats_.n_device_ops += 1;
+  s = dev_->Allreduce(src, dst, spec.count, spec.dtype, spec.op, MakeProbe());
+  if (s != Status::kSuccess) return s;
+  return dev_->Finish(MakeProbe());
+}
+
+Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
+  if (size == 0 || GetWorldSize() == 1) return Status::kSuccess;
+  if (!OnDevice(buf)) return host_->TreeBroadcast(buf, size, root);
+  Status s = EnsureDeviceComm();
+  if (s != Status::kSuccess) return s;
+  stats_.n_device_ops += 1;
+  dev_->EnterFromUser();
+  s = dev_->Broadcast(buf, size, root, MakeProbe());
+  if (s != Status::kSuccess) return s;
+  return dev_->Finish(MakeProbe());
+}
+
+Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t end,
+                                size_t prev_size) {
+  if (total == 0 || GetWorldSize() == 1) return Status::kSuccess;
+  if (!OnDevice(buf)) return host_->RingAllgather(buf, total, begin, end, prev_size);
+  // every rank needs every slice: exchange (begin, size) pairs over the host ring first
+  const int n = GetWorldSize();
+  std::vector<uint64_t> meta(2 * n, 0);
+  meta[2 * rank_] = begin;
+  meta[2 * rank_ + 1] = end - begin;
+  Status s = host_->RingAllgather(meta.data(), meta.size() * 8, 16 * rank_, 16 * rank_ + 16, 16);
+  if (s != Status::kSuccess) return s;
+  std::vector<size_t> b(n), z(n);
+  for (int r = 0; r < n; ++r) {
+    b[r] = static_cast<size_t>(meta[2 * r]);
+    z[r] = static_cast<size_t>(meta[2 * r + 1]);
+  }
+  s = EnsureDeviceComm();
+  if (s != Status::kSuccess) return s;
+  stats_.n_device_ops += 1;
+  dev_->EnterFromUser();
+  s = dev_->AllgatherV(buf, total, b, z, MakeProbe());
+  if (s != Status::kSuccess) return s;
+  return dev_->Finish(MakeProbe());
+}
+
+void EngineBase::Allreduce(void *buf, size_t type_nbytes, size_t count, ReduceFunction reducer,
+                           PreprocFunction prepare_fun, void *prepare_arg, const char *,
+                           const int, const char *) {
+  if (prepare_fun != nullptr) prepare_fun(prepare_arg);
+  if (GetWorldSize() == 1 && world1_fastpath_) return;
+  ReduceSpec spec;
+  spec.type_nbytes = type_nbytes;
+  spec.count = count;
+  spec.host_red = reducer;
+  const double t0 = utils::GetTime();
+  Status s = OnDevice(buf) ? TryAllreduceDevice(buf, buf, spec) : TryAllreduceHost(buf, spec);
+  utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));
+  stats_.n_allreduce += 1;
+  stats_.bytes_allreduce += static_cast<double>(spec.bytes());
+  stats_.t_allreduce += utils::GetTime() - t0;
+}
+
+void EngineBase::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, mpi::OpType op,
+                                ReduceFunction reducer, PreprocFunction prepare_fun,
+                                void *prepare_arg, const char *, const int, const char *) {
+  if (prepare_fun != nullptr) prepare_fun(prepare_arg);
+  if (GetWorldSize() == 1 && world1_fastpath_) return;
+  ReduceSpec spec;
+  spec.type_nbytes = coll::DTypeSize(dtype);
+  spec.count = count;
+  spec.host_red = reducer;
+  spec.dtype = dtype;
+  spec.op = op;
+  const double t0 = utils::GetTime();
+  Status s = OnDevice(buf) ? TryAllreduceDevice(buf, buf, spec) : TryAllreduceHost(buf, spec);
+  utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));
+  stats_.n_allreduce += 1;
+  stats_.bytes_allreduce += static_cast<double>(spec.bytes());
+  stats_.t_allreduce += utils::GetTime() - t0;
+}
+
+void EngineBase::DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype,
+                                      int op, int prep, double alpha, const char *, const int,
+                                      const char *) {
+  utils::Check(OnDevice(dst) && OnDevice(src), "DevAllreducePrepared needs device buffers");
+  dev_->EnterFromUser();
+  device::CheckHip(device::LaunchPrepare(dst, nullptr, src, count, dtype, prep, alpha,
+                                         dev_->stream()),
+                   "LaunchPrepare");
+  if (GetWorldSize() == 1 && world1_fastpath_) {
+    utils::Check(dev_->Finish(MakeProbe()) == Status::kSuccess, "prepare failed");
+    return;
+  }
+  ReduceSpec spec;
+  spec.type_nbytes = coll::DTypeSize(static_cast<mpi::DataType>(dtype));
+  spec.count = count;
+  spec.dtype = dtype;
+  spec.op = op;
+  Status s = TryAllreduceDevice(dst, dst, spec);
+  utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));
+  stats_.n_allreduce += 1;
+}
+
+void EngineBase::Broadcast(void *buf, size_t size, int root, const char *, const int,
+                           const char *) {
+  if (GetWorldSize() == 1) return;
+  const double t0 = utils::GetTime();
+  Status s = TryBroadcast(buf, size, root);
+  utils::Check(s == Status::kSuccess, "Broadcast failed: %s", net::StatusName(s));
+  stats_.n_broadcast += 1;
+  stats_.bytes_broadcast += static_cast<double>(size);
+  stats_.t_broadcast += utils::GetTime() - t0;
+}
+
+void EngineBase::Allgather(void *buf, size_t total, size_t begin, size_t end, size_t prev_size,
+                           const char *, const int, const char *) {
+  if (GetWorldSize() == 1) return;
+  const double t0 = utils::GetTime();
+  Status s = TryAllgather(buf, total, begin, end, prev_size);
+  utils::Check(s == Status::kSuccess, "Allgather failed: %s", net::StatusName(s));
+  stats_.n_allgather += 1;
+  stats_.bytes_allgather += static_cast<double>(total);
+  stats_.t_allgather += utils::GetTime() - t0;
+}
+
+int EngineBase::LoadCheckPoint(Serializable *, Serializable *) { return 0; }
+
+void EngineBase::CheckPoint(const Serializable *, const Serializable *) {
+  version_number_ += 1;
+  stats_.n_checkpoint += 1;
+}
+
+void EngineBase::LazyCheckPoint(const Serializable *) {
+  version_number_ += 1;
+  stats_.n_checkpoint += 1;
+}
+
+std::string EngineBase::StatsJson() const {
+  std::ostringstream os;
+  const EngineStats &s = stats_;
+  os << "{\"engine\":\"" << EngineName() << "\",\"rank\":" << rank_
+     << ",\"world_size\":" << GetWorldSize() << ",\"version\":" << version_number_
+     << ",\"device\":" << GetDevice() << ",\"device_epoch\":" << (dev_ ? dev_->epoch() : 0)
+     << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
+     << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
+     << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
+     << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
+     << ",\"n_consensus_elided\":" << s.n_consensus_elided
+     << ",\"bytes_allreduce\":" << s.bytes_allreduce
+     << ",\"bytes_broadcast\":" << s.bytes_broadcast
+     << ",\"bytes_allgather\":" << s.bytes_allgather << ",\"t_allreduce\":" << s.t_allreduce
+     << ",\"t_broadcast\":" << s.t_broadcast << ",\"t_allgather\":" << s.t_allgather
+     << ",\"t_checkpoint\":" << s.t_checkpoint << ",\"t_consensus\":" << s.t_consensus
+     << ",\"t_recover\":" << s.t_recover
+     << ",\"device_log_bytes\":" << (dev_ ? dev_->arena()->used() : 0) << "}";
+  return os.str();
+}
+}  // namespace engine
+}  // namespace rabit

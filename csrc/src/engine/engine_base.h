@@ -1,0 +1,151 @@
+/*!
+ * \file engine_base.h
+ * \brief Non-fault-tolerant engine: tracker client + host TCP plane + device RCCL plane.
+ *
+ * Parity: reference AllreduceBase (`src/allreduce_base.{h,cc}`).  The data path is chosen
+ * per call from the buffer's memory kind: host buffers use the TCP algorithms of
+ * coll::HostCollectives, HBM buffers use device::DevicePlane (RCCL over xGMI + gfx950
+ * kernels).  Every primitive returns a net::Status so the robust engine can retry.
+ */
+#ifndef XRABIT_ENGINE_ENGINE_BASE_H_
+#define XRABIT_ENGINE_ENGINE_BASE_H_
+
+#include <atomic>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "coll/host_coll.h"
+#include "device/device_plane.h"
+#include "net/links.h"
+#include "net/tracker_client.h"
+#include "rabit/internal/engine.h"
+
+namespace rabit {
+namespace engine {
+
+using net::Status;
+typedef IEngine::ReduceFunction *ReduceFn;
+
+/*! \brief per-engine counters exported by RabitGetStats */
+struct EngineStats {
+  uint64_t n_allreduce{0}, n_broadcast{0}, n_allgather{0}, n_checkpoint{0};
+  uint64_t n_device_ops{0}, n_recovered_ops{0}, n_recover_events{0}, n_consensus{0};
+  uint64_t n_consensus_elided{0};
+  double bytes_allreduce{0}, bytes_broadcast{0}, bytes_allgather{0};
+  double t_allreduce{0}, t_broadcast{0}, t_allgather{0}, t_checkpoint{0}, t_consensus{0};
+  double t_recover{0};
+};
+
+class EngineBase : public IEngine {
+ public:
+  EngineBase();
+  ~EngineBase() override;
+  /*! \brief parse params, connect to the tracker, bring up links and (lazily) the device */
+  virtual bool Init(int argc, char *argv[]);
+  /*! \brief close links, tell the tracker */
+  virtual bool Shutdown();
+  /*! \brief set one parameter (subclasses chain to the parent) */
+  virtual void SetParam(const char *name, const char *val);
+
+  void Allgather(void *sendrecvbuf, size_t total_size, size_t slice_begin, size_t slice_end,
+                 size_t size_prev_slice, const char *_file, const int _line,
+                 const char *_caller) override;
+  void Allreduce(void *sendrecvbuf_, size_t type_nbytes, size_t count, ReduceFunction reducer,
+                 PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                 const int _line, const char *_caller) override;
+  void AllreduceTyped(void *sendrecvbuf_, size_t count, mpi::DataType dtype, mpi::OpType op,
+                      ReduceFunction reducer, PreprocFunction prepare_fun, void *prepare_arg,
+                      const char *_file, const int _line, const char *_caller) override;
+  void Broadcast(void *sendrecvbuf_, size_t size, int root, const char *_file, const int _line,
+                 const char *_caller) override;
+  void InitAfterException() override {}
+  int LoadCheckPoint(Serializable *global_model, Serializable *local_model) override;
+  void CheckPoint(const Serializable *global_model, const Serializable *local_model) override;
+  void LazyCheckPoint(const Serializable *global_model) override;
+  int VersionNumber() const override { return version_number_; }
+  int GetRingPrevRank() const override;
+  int GetRank() const override { return rank_; }
+  int GetWorldSize() const override { return world_size_ == -1 ? 1 : world_size_; }
+  bool IsDistributed() const override { return tracker_.uri != "NULL"; }
+  std::string GetHost() const override { return host_uri_; }
+  void TrackerPrint(const std::string &msg) override;
+  void SetStream(void *stream) override;
+  int GetDevice() const override { return dev_ ? dev_->device() : -1; }
+  bool IsDevicePointer(const void *ptr) const override { return OnDevice(ptr); }
+  const char *EngineName() const override { return "base"; }
+
+  /*!
+   * \brief fused lazy-prepare allreduce of a device buffer: dst = prep(src) then
+   *        allreduce(dst).  The base engine always runs the prepare kernel.
+   */
+  virtual void DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype, int op,
+                                    int prep, double alpha, const char *_file, const int _line,
+                                    const char *_caller);
+  /*! \brief engine statistics as JSON */
+  virtual std::string StatsJson() const;
+  device::DevicePlane *device_plane() { return dev_.get(); }
+
+ protected:
+  /*! \brief how to reduce: element size/count plus either a built-in (dtype, op) or a
+   *  host reduce function */
+  struct ReduceSpec {
+    size_t type_nbytes{1};
+    size_t count{0};
+    ReduceFn host_red{nullptr};
+    int dtype{-1};
+    int op{-1};
+    size_t bytes() const { return type_nbytes * count; }
+    bool builtin() const { return dtype >= 0 && op >= 0; }
+  };
+  bool OnDevice(const void *p) const;
+  /*! \brief in-place allreduce over the host plane */
+  Status TryAllreduceHost(void *buf, const ReduceSpec &spec);
+  /*!
+   * \brief device allreduce dst = reduce(src) (src may equal dst); custom host reducers are
+   *        staged through host memory
+   */
+  Status TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec);
+  Status TryBroadcast(void *buf, size_t size, int root);
+  Status TryAllgather(void *buf, size_t total, size_t begin, size_t end, size_t prev_size);
+  /*! \brief build the RCCL communicator if missing (collective) */
+  Status EnsureDeviceComm();
+  /*! \brief (re)connect peer links through the tracker */
+  bool ReconnectLinks(const char *cmd);
+  /*! \brief true if any peer link hung up (used while waiting on device ops) */
+  bool PeerFailureProbe() const;
+  /*! \brief Hadoop status line */
+  void ReportStatus() const;
+  device::FailureProbe MakeProbe() const {
+    return [this]() { return this->PeerFailureProbe(); };
+  }
+
+  // parameters / configuration
+  std::vector<std::string> env_vars_;
+  net::TrackerConfig tracker_;
+  coll::HostCollConfig hcfg_;
+  device::DeviceConfig dcfg_;
+  int device_plane_mode_{1};  // 0: never, 1: when a GPU is visible
+  std::string dmlc_role_{"worker"};
+  std::string host_uri_;
+  bool hadoop_mode_{false};
+  bool debug_{false};
+  bool bootstrap_cache_{false};
+  bool timeout_enabled_{false};
+  int timeout_sec_{1800};
+  bool world1_fastpath_{true};
+  // runtime state
+  net::Topology topo_;
+  std::unique_ptr<coll::HostCollectives> host_;
+  std::unique_ptr<device::DevicePlane> dev_;
+  void *user_stream_{nullptr};
+  std::atomic<bool> abort_flag_{false};
+  int rank_{0};
+  int world_size_{-1};
+  int version_number_{0};
+  int seq_counter_{0};
+  EngineStats stats_;
+};
+}  // namespace engine
+}  // namespace rabit
+#endif  // XRABIT_ENGINE_ENGINE_BASE_H_

@@ -1,0 +1,608 @@
+/*!
+ * \file engine_robust.cc
+ * \brief Fault-tolerant engine: collectives, checkpoints, result log, bootstrap cache,
+ *        watchdog.  The recovery protocol itself is in recovery.cc.
+ */
+#include "engine/engine_robust.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "device/kernels.h"
+#include "rabit/internal/io.h"
+#include "rabit/internal/timer.h"
+#include "rabit/internal/utils.h"
+
+namespace rabit {
+namespace engine {
+
+// ------------------------------------------------------------------ ResultLog
+void EngineRobust::ResultLog::Clear() {
+  entries_.clear();
+  host_used_ = 0;
+  if (arena_ != nullptr) arena_->Reset();
+}
+
+void *EngineRobust::ResultLog::AllocTemp(size_t size, bool device) {
+  utils::Assert(size != 0, "cannot log a zero-size result");
+  temp_ = Entry{-1, size, device, 0, nullptr};
+  if (device) {
+    utils::Check(arena_ != nullptr, "device result without a device arena");
+    void *p = arena_->Alloc(size);
+    utils::Check(p != nullptr,
+                 "device result log is full (%zu bytes logged since the last checkpoint); "
+                 "checkpoint more often or raise rabit_device_log_cap",
+                 arena_->used());
+    temp_.dev_ptr = p;
+    return p;
+  }
+  const size_t words = (size + 7) / 8;
+  if (host_.size() < host_used_ + words) host_.resize(std::max(host_used_ + words, host_.size() * 2));
+  temp_.host_off = host_used_;
+  return host_.data() + host_used_;
+}
+
+void EngineRobust::ResultLog::PushTemp(int seqno, size_t size) {
+  utils::Assert(size == temp_.size, "PushTemp: size differs from AllocTemp");
+  if (!entries_.empty()) {
+    utils::Assert(entries_.back().seqno < seqno, "PushTemp: sequence numbers must increase");
+  }
+  temp_.seqno = seqno;
+  entries_.push_back(temp_);
+  if (!temp_.on_device) host_used_ += (size + 7) / 8;
+}
+
+const EngineRobust::ResultLog::Entry *EngineRobust::ResultLog::Query(int seqno) const {
+  auto it = std::lower_bound(entries_.begin(), entries_.end(), seqno,
+                             [](const Entry &e, int s) { return e.seqno < s; });
+  if (it == entries_.end() || it->seqno != seqno) return nullptr;
+  return &*it;
+}
+
+void EngineRobust::ResultLog::DropLast() {
+  utils::Assert(!entries_.empty(), "nothing to drop");
+  const Entry e = entries_.back();
+  entries_.pop_back();
+  if (e.on_device) {
+    if (arena_ != nullptr) arena_->PopTo(e.dev_ptr);
+  } else {
+    host_used_ = e.host_off;
+  }
+}
+
+// ------------------------------------------------------------------ consensus reducer
+void EngineRobust::ActionSummary::Reducer(const void *src_, void *dst_, int len,
+                                          const MPI::Datatype &) {
+  const ActionSummary *src = static_cast<const ActionSummary *>(src_);
+  ActionSummary *dst = static_cast<ActionSummary *>(dst_);
+  for (int i = 0; i < len; ++i) {
+    const uint32_t min_seq = std::min(src[i].seqno(), dst[i].seqno());
+    const uint32_t max_cache = std::max(src[i].seqno(kCache), dst[i].seqno(kCache));
+    const int flags = src[i].flag() | dst[i].flag() |
+                      (src[i].seqno() != dst[i].seqno() ? kDiffSeq : 0);
+    const int role = src[i].flag(kCache) & dst[i].flag(kCache);
+    dst[i] = ActionSummary(flags, role, min_seq, max_cache);
+  }
+}
+
+// ------------------------------------------------------------------ lifecycle
+EngineRobust::EngineRobust() {
+  env_vars_.push_back("rabit_global_replica");
+  env_vars_.push_back("rabit_local_replica");
+}
+
+EngineRobust::~EngineRobust() { StopWatchdog(); }
+
+void EngineRobust::SetParam(const char *name, const char *val) {
+  EngineBase::SetParam(name, val);
+  if (!strcmp(name, "rabit_global_replica")) num_global_replica_ = atoi(val);
+  if (!strcmp(name, "rabit_local_replica")) num_local_replica_ = atoi(val);
+  if (!strcmp(name, "rabit_elide_consensus")) elide_consensus_ = utils::StringToBool(val);
+}
+
+bool EngineRobust::Init(int argc, char *argv[]) {
+  if (!EngineBase::Init(argc, argv)) return false;
+  if (bootstrap_cache_) utils::HandleLogInfo("[EXPERIMENTAL] bootstrap cache enabled\n");
+  checkpoint_loaded_ = false;
+  result_buffer_round_ =
+      num_global_replica_ == 0 ? -1 : std::max(GetWorldSize() / num_global_replica_, 1);
+  if (dev_) resbuf_.SetArena(dev_->arena());
+  if (timeout_enabled_) StartWatchdog();
+  return true;
+}
+
+bool EngineRobust::Shutdown() {
+  try {
+    if (GetWorldSize() > 1 || !world1_fastpath_) {
+      // a pseudo checkpoint keeps serving late / recovering peers before everyone leaves
+      utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckPoint, ActionSummary::kSpecialOp,
+                               cur_cache_seq_, "Shutdown"),
+                   "Shutdown: checkpoint must return true");
+      resbuf_.Clear();
+      seq_counter_ = 0;
+      cachebuf_.Clear();
+      cur_cache_seq_ = 0;
+      lookupbuf_.Clear();
+      utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckAck, ActionSummary::kSpecialOp,
+                               cur_cache_seq_, "Shutdown"),
+                   "Shutdown: check ack must return true");
+    }
+    recovering_since_.store(0.0);
+    StopWatchdog();
+    return EngineBase::Shutdown();
+  } catch (const std::exception &e) {
+    fprintf(stderr, "xrabit: shutdown failed: %s\n", e.what());
+    return false;
+  }
+}
+
+void EngineRobust::InitAfterException() {
+  // drop every link and rejoin through the tracker, as after a failure
+  for (auto &l : topo_.links) l->sock.Close();
+  if (dev_) dev_->AbortComm();
+  fast_mode_ = false;
+  ReconnectLinks("recover");
+}
+
+// ------------------------------------------------------------------ helpers
+void EngineRobust::ApplyRetention() {
+  const int last = resbuf_.LastSeqNo();
+  if (last != -1 &&
+      (result_buffer_round_ == -1 || last % result_buffer_round_ != rank_ % result_buffer_round_)) {
+    resbuf_.DropLast();
+  }
+}
+
+void EngineRobust::CopyAny(void *dst, bool dst_dev, const void *src, bool src_dev, size_t n) {
+  if (n == 0 || dst == src) return;
+  if (!dst_dev && !src_dev) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  dev_->EnterFromUser();
+  dev_->CopyAsync(dst, src, n);
+  utils::Check(dev_->Finish(MakeProbe(), true) == Status::kSuccess, "device copy failed");
+}
+
+// ------------------------------------------------------------------ collectives
+void EngineRobust::Allreduce(void *buf, size_t type_nbytes, size_t count,
+                             ReduceFunction reducer, PreprocFunction prepare_fun,
+                             void *prepare_arg, const char *_file, const int _line,
+                             const char *_caller) {
+  ReduceSpec spec;
+  spec.type_nbytes = type_nbytes;
+  spec.count = count;
+  spec.host_red = reducer;
+  AllreduceImpl(buf, spec, prepare_fun, prepare_arg, _file, _line, _caller);
+}
+
+void EngineRobust::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, mpi::OpType op,
+                                  ReduceFunction reducer, PreprocFunction prepare_fun,
+                                  void *prepare_arg, const char *_file, const int _line,
+                                  const char *_caller) {
+  ReduceSpec spec;
+  spec.type_nbytes = coll::DTypeSize(dtype);
+  spec.count = count;
+  spec.host_red = reducer;
+  spec.dtype = dtype;
+  spec.op = op;
+  AllreduceImpl(buf, spec, prepare_fun, prepare_arg, _file, _line, _caller);
+}
+
+void EngineRobust::DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype,
+                                        int op, int prep, double alpha, const char *_file,
+                                        const int _line, const char *_caller) {
+  utils::Check(OnDevice(dst) && OnDevice(src), "DevAllreducePrepared needs device buffers");
+  ReduceSpec spec;
+  spec.type_nbytes = coll::DTypeSize(static_cast<mpi::DataType>(dtype));
+  spec.count = count;
+  spec.dtype = dtype;
+  spec.op = op;
+  AllreduceImpl(dst, spec, nullptr, nullptr, _file, _line, _caller, src, prep, alpha);
+}
+
+void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunction prepare_fun,
+                                 void *prepare_arg, const char *_file, const int _line,
+                                 const char *_caller, const void *prep_src, int prep_op,
+                                 double prep_alpha) {
+  const bool dev = OnDevice(buf);
+  const size_t bytes = spec.bytes();
+  auto run_prepare = [&]() {
+    if (prep_src != nullptr) {
+      dev_->EnterFromUser();
+      device::CheckHip(device::LaunchPrepare(buf, nullptr, prep_src, spec.count, spec.dtype,
+                                             prep_op, prep_alpha, dev_->stream()),
+                       "LaunchPrepare");
+    } else if (prepare_fun != nullptr) {
+      prepare_fun(prepare_arg);
+    }
+  };
+  if (GetWorldSize() == 1 && world1_fastpath_) {
+    run_prepare();
+    if (prep_src != nullptr) dev_->Finish(MakeProbe(), false);
+    return;
+  }
+  if (bytes == 0) {
+    run_prepare();
+    return;
+  }
+  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
+                          "#" + std::to_string(spec.type_nbytes) + "x" +
+                          std::to_string(spec.count);
+  if (!checkpoint_loaded_ && bootstrap_cache_ && GetBootstrapCache(key, buf, bytes) != -1) {
+    return;
+  }
+  const double t0 = utils::GetTime();
+  bool recovered = RecoverExec(buf, bytes, 0, seq_counter_, cur_cache_seq_, "Allreduce");
+  ApplyRetention();
+  if (!recovered) run_prepare();
+  void *temp = resbuf_.AllocTemp(bytes, dev);
+  for (;;) {
+    if (recovered) {
+      CopyAny(temp, dev, buf, dev, bytes);
+      stats_.n_recovered_ops += 1;
+      break;
+    }
+    Status s;
+    if (dev) {
+      // RCCL reduces straight into the log slot; the user buffer keeps the input for retries
+      s = TryAllreduceDevice(buf, temp, spec);
+    } else {
+      std::memcpy(temp, buf, bytes);
+      s = TryAllreduceHost(temp, spec);
+    }
+    if (CheckAndRecover(s)) {
+      if (dev) {
+        dev_->CopyAsync(buf, temp, bytes);
+        dev_->Finish(MakeProbe(), false);  // local copy: order the user stream, no host wait
+      } else {
+        std::memcpy(buf, temp, bytes);
+      }
+      break;
+    }
+    recovered = RecoverExec(buf, bytes, 0, seq_counter_, cur_cache_seq_, "Allreduce");
+  }
+  const double dt = utils::GetTime() - t0;
+  stats_.n_allreduce += 1;
+  stats_.bytes_allreduce += static_cast<double>(bytes);
+  stats_.t_allreduce += dt;
+  if (debug_) {
+    utils::HandleLogInfo("[%d] allreduce (%s) finished version %d, seq %d, take %f seconds\n",
+                         rank_, key.c_str(), version_number_, seq_counter_, dt);
+  }
+  if (checkpoint_loaded_ || !bootstrap_cache_) {
+    resbuf_.PushTemp(seq_counter_, bytes);
+    seq_counter_ += 1;
+  } else {
+    resbuf_.PushTemp(seq_counter_, bytes);
+    resbuf_.DropLast();
+    SetBootstrapCache(key, buf, bytes);
+  }
+}
+
+void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char *_file,
+                             const int _line, const char *_caller) {
+  if (GetWorldSize() == 1 && world1_fastpath_) return;
+  if (total_size == 0) return;
+  const bool dev = OnDevice(buf);
+  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
+                          "#" + std::to_string(total_size) + "@" + std::to_string(root);
+  if (!checkpoint_loaded_ && bootstrap_cache_ &&
+      GetBootstrapCache(key, buf, total_size) != -1) {
+    return;
+  }
+  const double t0 = utils::GetTime();
+  bool recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Broadcast");
+  ApplyRetention();
+  void *temp = resbuf_.AllocTemp(total_size, dev);
+  for (;;) {
+    if (recovered) {
+      CopyAny(temp, dev, buf, dev, total_size);
+      stats_.n_recovered_ops += 1;
+      break;
+    }
+    if (CheckAndRecover(TryBroadcast(buf, total_size, root))) {
+      if (dev) {
+        dev_->CopyAsync(temp, buf, total_size);
+        dev_->Finish(MakeProbe(), false);
+      } else {
+        std::memcpy(temp, buf, total_size);
+      }
+      break;
+    }
+    recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Broadcast");
+  }
+  const double dt = utils::GetTime() - t0;
+  stats_.n_broadcast += 1;
+  stats_.bytes_broadcast += static_cast<double>(total_size);
+  stats_.t_broadcast += dt;
+  if (debug_) {
+    utils::HandleLogInfo(
+        "[%d] broadcast (%s) root %d finished version %d, seq %d, take %f seconds\n", rank_,
+        key.c_str(), root, version_number_, seq_counter_, dt);
+  }
+  if (checkpoint_loaded_ || !bootstrap_cache_) {
+    resbuf_.PushTemp(seq_counter_, total_size);
+    seq_counter_ += 1;
+  } else {
+    resbuf_.PushTemp(seq_counter_, total_size);
+    resbuf_.DropLast();
+    SetBootstrapCache(key, buf, total_size);
+  }
+}
+
+void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, size_t slice_end,
+                             size_t size_prev_slice, const char *_file, const int _line,
+                             const char *_caller) {
+  if (GetWorldSize() == 1 && world1_fastpath_) return;
+  if (total_size == 0) return;
+  const bool dev = OnDevice(buf);
+  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
+                          "#" + std::to_string(total_size);
+  if (!checkpoint_loaded_ && bootstrap_cache_ &&
+      GetBootstrapCache(key, buf, total_size) != -1) {
+    return;
+  }
+  const double t0 = utils::GetTime();
+  bool recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Allgather");
+  ApplyRetention();
+  void *temp = resbuf_.AllocTemp(total_size, dev);
+  for (;;) {
+    if (recovered) {
+      CopyAny(temp, dev, buf, dev, total_size);
+      stats_.n_recovered_ops += 1;
+      break;
+    }
+    // in place on the user buffer: the ring never overwrites this rank's own slice, so a
+    // retry after a failure still finds its input
+    if (CheckAndRecover(TryAllgather(buf, total_size, slice_begin, slice_end, size_prev_slice))) {
+      if (dev) {
+        dev_->CopyAsync(temp, buf, total_size);
+        dev_->Finish(MakeProbe(), false);
+      } else {
+        std::memcpy(temp, buf, total_size);
+      }
+      break;
+    }
+    recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Allgather");
+  }
+  const double dt = utils::GetTime() - t0;
+  stats_.n_allgather += 1;
+  stats_.bytes_allgather += static_cast<double>(total_size);
+  stats_.t_allgather += dt;
+  if (debug_) {
+    utils::HandleLogInfo("[%d] allgather (%s) finished version %d, seq %d, take %f seconds\n",
+                         rank_, key.c_str(), version_number_, seq_counter_, dt);
+  }
+  if (checkpoint_loaded_ || !bootstrap_cache_) {
+    resbuf_.PushTemp(seq_counter_, total_size);
+    seq_counter_ += 1;
+  } else {
+    resbuf_.PushTemp(seq_counter_, total_size);
+    resbuf_.DropLast();
+    SetBootstrapCache(key, buf, total_size);
+  }
+}
+
+// ------------------------------------------------------------------ checkpoints
+void EngineRobust::LocalModelCheck(bool with_local) {
+  if (use_local_model_ == -1) {
+    if (with_local) {
+      use_local_model_ = 1;
+      if (num_local_replica_ == 0) num_local_replica_ = default_local_replica_;
+    } else {
+      use_local_model_ = 0;
+      num_local_replica_ = 0;
+    }
+  } else {
+    utils::Check(use_local_model_ == static_cast<int>(with_local),
+                 "CheckPoint/LoadCheckPoint must always be called either with or without "
+                 "local_model, not both");
+  }
+}
+
+int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local_model) {
+  checkpoint_loaded_ = true;
+  if (GetWorldSize() == 1 && world1_fastpath_) return 0;
+  LocalModelCheck(local_model != nullptr);
+  if (num_local_replica_ == 0) {
+    utils::Check(local_model == nullptr,
+                 "need to set rabit_local_replica larger than 1 to checkpoint local_model");
+  }
+  const double t0 = utils::GetTime();
+  if (RecoverExec(nullptr, 0, ActionSummary::kLoadCheck, ActionSummary::kSpecialOp,
+                  cur_cache_seq_, "LoadCheckPoint")) {
+    const int nlocal =
+        std::max(static_cast<int>(local_rptr_[local_chkpt_version_].size()) - 1, 0);
+    if (local_model != nullptr) {
+      if (nlocal == num_local_replica_ + 1) {
+        utils::MemoryFixSizeBuffer fs(BeginPtr(local_chkpt_[local_chkpt_version_]),
+                                      local_rptr_[local_chkpt_version_][1]);
+        local_model->Load(&fs);
+      } else {
+        utils::Assert(nlocal == 0, "[%d] local model inconsistent, nlocal=%d", rank_, nlocal);
+      }
+    }
+    resbuf_.Clear();
+    seq_counter_ = 0;
+    utils::MemoryBufferStream fs(&global_checkpoint_);
+    if (global_checkpoint_.empty()) {
+      version_number_ = 0;
+    } else {
+      utils::Assert(fs.Read(&version_number_, sizeof(version_number_)) ==
+                        sizeof(version_number_),
+                    "read in version number");
+      global_model->Load(&fs);
+      utils::Assert(local_model == nullptr || nlocal == num_local_replica_ + 1,
+                    "local model inconsistent, nlocal=%d", nlocal);
+    }
+    utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckAck, ActionSummary::kSpecialOp,
+                             cur_cache_seq_, "LoadCheckPoint"),
+                 "check ack must return true");
+    if (!RecoverExec(nullptr, 0, ActionSummary::kLoadBootstrapCache, seq_counter_,
+                     cur_cache_seq_, "LoadCheckPoint") &&
+        debug_) {
+      utils::HandleLogInfo("[%d] no bootstrap cache to load\n", rank_);
+    }
+    if (debug_) {
+      utils::HandleLogInfo(
+          "[%d] loadcheckpoint size %zu finished version %d, seq %d, take %f seconds\n", rank_,
+          global_checkpoint_.length(), version_number_, seq_counter_, utils::GetTime() - t0);
+    }
+    return version_number_;
+  }
+  if (debug_) utils::HandleLogInfo("[%d] loadcheckpoint reset\n", rank_);
+  resbuf_.Clear();
+  seq_counter_ = 0;
+  version_number_ = 0;
+  return version_number_;
+}
+
+void EngineRobust::CheckPointImpl(const Serializable *global_model,
+                                  const Serializable *local_model, bool lazy) {
+  if (GetWorldSize() == 1 && world1_fastpath_) {
+    version_number_ += 1;
+    return;
+  }
+  const double t0 = utils::GetTime();
+  LocalModelCheck(local_model != nullptr);
+  if (num_local_replica_ == 0) {
+    utils::Check(local_model == nullptr,
+                 "need to set rabit_local_replica larger than 1 to checkpoint local_model");
+  }
+  if (num_local_replica_ != 0) {
+    for (;;) {
+      if (RecoverExec(nullptr, 0, 0, ActionSummary::kLocalCheckPoint, cur_cache_seq_,
+                      "CheckPoint")) {
+        break;
+      }
+      const int nv = !local_chkpt_version_;
+      local_chkpt_[nv].clear();
+      utils::MemoryBufferStream fs(&local_chkpt_[nv]);
+      if (local_model != nullptr) local_model->Save(&fs);
+      local_rptr_[nv].clear();
+      local_rptr_[nv].push_back(0);
+      local_rptr_[nv].push_back(local_chkpt_[nv].length());
+      if (CheckAndRecover(TryCheckinLocalState(&local_rptr_[nv], &local_chkpt_[nv]))) break;
+    }
+    RecoverExec(nullptr, 0, 0, ActionSummary::kLocalCheckAck, cur_cache_seq_, "CheckPoint");
+    local_chkpt_version_ = !local_chkpt_version_;
+  }
+  utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckPoint, ActionSummary::kSpecialOp,
+                           cur_cache_seq_, "CheckPoint"),
+               "check point must return true");
+  version_number_ += 1;
+  if (lazy) {
+    global_lazycheck_ = global_model;
+  } else {
+    global_checkpoint_.clear();
+    utils::MemoryBufferStream fs(&global_checkpoint_);
+    fs.Write(&version_number_, sizeof(version_number_));
+    global_model->Save(&fs);
+    global_lazycheck_ = nullptr;
+  }
+  if (debug_) {
+    utils::HandleLogInfo("[%d] checkpoint finished version %d, seq %d, take %f seconds\n", rank_,
+                         version_number_, seq_counter_, utils::GetTime() - t0);
+  }
+  const double t1 = utils::GetTime();
+  resbuf_.Clear();
+  seq_counter_ = 0;
+  utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckAck, ActionSummary::kSpecialOp,
+                           cur_cache_seq_, "CheckPoint"),
+               "check ack must return true");
+  if (debug_) {
+    utils::HandleLogInfo("[%d] checkpoint ack finished version %d, take %f seconds\n", rank_,
+                         version_number_, utils::GetTime() - t1);
+  }
+  stats_.n_checkpoint += 1;
+  stats_.t_checkpoint += utils::GetTime() - t0;
+}
+
+// ------------------------------------------------------------------ bootstrap cache
+int EngineRobust::SetBootstrapCache(const std::string &key, const void *buf, size_t nbytes) {
+  utils::Assert(nbytes > 0, "can't set empty cache");
+  const bool dev = OnDevice(buf);
+  void *temp = cachebuf_.AllocTemp(nbytes, false);
+  if (dev) {
+    dev_->StageToHost(temp, buf, nbytes);
+  } else {
+    std::memcpy(temp, buf, nbytes);
+  }
+  cachebuf_.PushTemp(cur_cache_seq_, nbytes);
+  void *name = lookupbuf_.AllocTemp(key.size() + 1, false);
+  std::memcpy(name, key.c_str(), key.size() + 1);
+  lookupbuf_.PushTemp(cur_cache_seq_, key.size() + 1);
+  cur_cache_seq_ += 1;
+  return 0;
+}
+
+int EngineRobust::GetBootstrapCache(const std::string &key, void *buf, size_t nbytes) {
+  if (!RecoverExec(nullptr, 0, ActionSummary::kLoadBootstrapCache, seq_counter_, cur_cache_seq_,
+                   "GetBootstrapCache")) {
+    return -1;
+  }
+  int index = -1;
+  for (int i = 0; i < cur_cache_seq_; ++i) {
+    const ResultLog::Entry *e = lookupbuf_.Query(i);
+    if (e != nullptr && e->size == key.size() + 1 &&
+        strcmp(static_cast<const char *>(lookupbuf_.Data(*e)), key.c_str()) == 0) {
+      index = i;
+      break;
+    }
+  }
+  if (index == -1) return -1;
+  const ResultLog::Entry *e = cachebuf_.Query(index);
+  utils::Assert(e != nullptr && e->size == nbytes, "cached size differs from the request");
+  void *src = cachebuf_.Data(*e);
+  if (OnDevice(buf)) {
+    dev_->StageToDevice(buf, src, nbytes);
+  } else {
+    std::memcpy(buf, src, nbytes);
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ watchdog
+void EngineRobust::StartWatchdog() {
+  if (watchdog_.joinable()) return;
+  wd_stop_ = false;
+  watchdog_ = std::thread([this]() { WatchdogLoop(); });
+}
+
+void EngineRobust::StopWatchdog() {
+  if (!watchdog_.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(wd_mu_);
+    wd_stop_ = true;
+  }
+  wd_cv_.notify_all();
+  watchdog_.join();
+}
+
+void EngineRobust::WatchdogLoop() {
+  std::unique_lock<std::mutex> lk(wd_mu_);
+  while (!wd_stop_) {
+    wd_cv_.wait_for(lk, std::chrono::milliseconds(100));
+    if (wd_stop_) break;
+    const double since = recovering_since_.load();
+    if (since > 0 && utils::GetTime() - since > timeout_sec_ && !watchdog_fired_.load()) {
+      watchdog_fired_.store(true);
+      // unblock whatever this rank is waiting on, then apply the timeout action
+      abort_flag_.store(true);
+      if (timeout_handler_ != nullptr) {
+        timeout_handler_(rank_, timeout_sec_);
+      } else {
+        fprintf(stderr, "[%d] xrabit: recovery did not finish within %d s, exiting\n", rank_,
+                timeout_sec_);
+        fflush(stderr);
+        std::_Exit(253);
+      }
+    }
+  }
+}
+}  // namespace engine
+}  // namespace rabit

@@ -1,0 +1,223 @@
+/*!
+ * \file engine_robust.h
+ * \brief Fault-tolerant engine: consensus, result log, checkpoints and replay recovery.
+ *
+ * Parity: reference AllreduceRobust (`src/allreduce_robust.{h,cc}`, `allreduce_robust-inl.h`).
+ * Semantics kept: every collective is identified by (version, seqno); a restarted worker
+ * reloads the last checkpoint from peers and replays the results of every collective since
+ * then from the peers' result logs, without re-running its lazy prepare functions; survivors
+ * block and serve it.  MI355X-specific design:
+ *  - results of HBM collectives are logged in an HBM arena (no host round trip on the hot
+ *    path); RCCL writes the result straight into its log slot (out-of-place), then one D2D
+ *    copy lands it in the user buffer;
+ *  - the per-op consensus round is elided in steady state (all ranks agreed on "execute" at
+ *    the previous op and nobody has seen a failure since); any failure or special action
+ *    (checkpoint, load, bootstrap cache) re-enables it, so the replay protocol is unchanged;
+ *  - a real watchdog: on timeout it aborts the device communicator and the process instead
+ *    of throwing into a discarded future (reference quirk).
+ */
+#ifndef XRABIT_ENGINE_ENGINE_ROBUST_H_
+#define XRABIT_ENGINE_ENGINE_ROBUST_H_
+
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine/engine_base.h"
+
+namespace rabit {
+namespace engine {
+
+class EngineRobust : public EngineBase {
+ public:
+  EngineRobust();
+  ~EngineRobust() override;
+  bool Init(int argc, char *argv[]) override;
+  bool Shutdown() override;
+  void SetParam(const char *name, const char *val) override;
+
+  void Allgather(void *sendrecvbuf, size_t total_size, size_t slice_begin, size_t slice_end,
+                 size_t size_prev_slice, const char *_file, const int _line,
+                 const char *_caller) override;
+  void Allreduce(void *sendrecvbuf_, size_t type_nbytes, size_t count, ReduceFunction reducer,
+                 PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                 const int _line, const char *_caller) override;
+  void AllreduceTyped(void *sendrecvbuf_, size_t count, mpi::DataType dtype, mpi::OpType op,
+                      ReduceFunction reducer, PreprocFunction prepare_fun, void *prepare_arg,
+                      const char *_file, const int _line, const char *_caller) override;
+  void Broadcast(void *sendrecvbuf_, size_t total_size, int root, const char *_file,
+                 const int _line, const char *_caller) override;
+  void InitAfterException() override;
+  int LoadCheckPoint(Serializable *global_model, Serializable *local_model) override;
+  void CheckPoint(const Serializable *global_model, const Serializable *local_model) override {
+    CheckPointImpl(global_model, local_model, false);
+  }
+  void LazyCheckPoint(const Serializable *global_model) override {
+    CheckPointImpl(global_model, nullptr, true);
+  }
+  const char *EngineName() const override { return "robust"; }
+  void DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype, int op,
+                            int prep, double alpha, const char *_file, const int _line,
+                            const char *_caller) override;
+
+  // ---- hooks used by unit tests (white-box)
+  /*! \brief called when the watchdog expires (default: log and terminate the process) */
+  typedef void (*TimeoutHandler)(int rank, int timeout_sec);
+  void SetTimeoutHandler(TimeoutHandler h) { timeout_handler_ = h; }
+  /*! \brief feed CheckAndRecover directly (tests); returns its result */
+  bool TestCheckAndRecover(Status s) { return CheckAndRecover(s); }
+  bool watchdog_fired() const { return watchdog_fired_.load(); }
+  bool consensus_elided() const { return fast_mode_; }
+
+ protected:
+  /*! \brief role of a node in a recovery transfer */
+  enum RecoverType { kHaveData = 0, kRequestData = 1, kPassData = 2 };
+  enum SeqType { kSeq = 0, kCache = 1 };
+
+  /*!
+   * \brief 8-byte consensus message (reference allreduce_robust.h:224-322):
+   *   seqcode    = (min seqno << 5) | action flags
+   *   maxseqcode = (max bootstrap-cache seqno << 5) | cache-role flag
+   */
+  struct ActionSummary {
+    static constexpr uint32_t kSpecialOp = 1u << 26;
+    static constexpr uint32_t kLocalCheckPoint = (1u << 26) - 2;
+    static constexpr uint32_t kLocalCheckAck = (1u << 26) - 1;
+    static constexpr int kLoadCheck = 1;
+    static constexpr int kCheckPoint = 2;
+    static constexpr int kCheckAck = 4;
+    static constexpr int kDiffSeq = 8;
+    static constexpr int kLoadBootstrapCache = 16;
+    uint32_t seqcode{0}, maxseqcode{0};
+    ActionSummary() = default;
+    ActionSummary(int flag, int cache_flag, uint32_t minseqno = kSpecialOp,
+                  uint32_t maxseqno = kSpecialOp)
+        : seqcode((minseqno << 5) | static_cast<uint32_t>(flag)),
+          maxseqcode((maxseqno << 5) | static_cast<uint32_t>(cache_flag)) {}
+    uint32_t code(SeqType t) const { return t == kSeq ? seqcode : maxseqcode; }
+    uint32_t seqno(SeqType t = kSeq) const { return code(t) >> 5; }
+    int flag(SeqType t = kSeq) const { return static_cast<int>(code(t) & 31); }
+    bool load_check(SeqType t = kSeq) const { return (code(t) & kLoadCheck) != 0; }
+    bool load_cache(SeqType t = kSeq) const { return (code(t) & kLoadBootstrapCache) != 0; }
+    bool check_point(SeqType t = kSeq) const { return (code(t) & kCheckPoint) != 0; }
+    bool check_ack(SeqType t = kSeq) const { return (code(t) & kCheckAck) != 0; }
+    bool diff_seq() const { return (seqcode & kDiffSeq) != 0; }
+    static void Reducer(const void *src, void *dst, int len, const MPI::Datatype &);
+  };
+
+  /*!
+   * \brief append-only log of collective results since the last checkpoint; each entry lives
+   *        in host memory or in the HBM arena of the device plane
+   */
+  class ResultLog {
+   public:
+    struct Entry {
+      int seqno;
+      size_t size;
+      bool on_device;
+      size_t host_off;  // in uint64 words
+      void *dev_ptr;
+    };
+    void SetArena(device::DeviceArena *a) { arena_ = a; }
+    void Clear();
+    /*! \brief scratch slot for the next result (not visible until PushTemp) */
+    void *AllocTemp(size_t size, bool device);
+    void PushTemp(int seqno, size_t size);
+    /*! \brief stored entry for seqno or nullptr */
+    const Entry *Query(int seqno) const;
+    void *Data(const Entry &e) {
+      return e.on_device ? e.dev_ptr : static_cast<void *>(host_.data() + e.host_off);
+    }
+    void DropLast();
+    int LastSeqNo() const { return entries_.empty() ? -1 : entries_.back().seqno; }
+    size_t size() const { return entries_.size(); }
+
+   private:
+    std::vector<Entry> entries_;
+    std::vector<uint64_t> host_;
+    size_t host_used_{0};
+    Entry temp_{};
+    device::DeviceArena *arena_{nullptr};
+  };
+
+  // ---- collectives
+  void AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunction prepare_fun,
+                     void *prepare_arg, const char *_file, const int _line, const char *_caller,
+                     const void *prep_src = nullptr, int prep_op = 0, double prep_alpha = 0);
+  void CheckPointImpl(const Serializable *global_model, const Serializable *local_model,
+                      bool lazy);
+  /*! \brief drop the previous result unless this rank is one of its replicas */
+  void ApplyRetention();
+  /*! \brief copy n bytes between host/device locations (synchronous w.r.t. the result) */
+  void CopyAny(void *dst, bool dst_dev, const void *src, bool src_dev, size_t n);
+
+  // ---- recovery protocol
+  /*!
+   * \brief run recovery actions preceding the requested one
+   * \return true if the request was satisfied by recovery (buf holds the result),
+   *         false if this is the newest action and must be executed
+   */
+  bool RecoverExec(void *buf, size_t size, int flag, int seqno, int cache_seqno,
+                   const char *caller = "RecoverExec");
+  /*! \brief true on success; on error repair links (tracker "recover") and return false */
+  bool CheckAndRecover(Status s);
+  Status TryLoadCheckPoint(bool requester);
+  Status TryGetResult(void *buf, size_t size, int seqno, bool requester);
+  Status TryDecideRouting(RecoverType role, size_t *p_size, int *p_recvlink,
+                          std::vector<bool> *p_req_in);
+  Status TryRecoverData(RecoverType role, void *buf, size_t size, int recv_link,
+                        const std::vector<bool> &req_in);
+  Status TryRestoreCache(bool requester, int min_seq, int max_seq);
+  Status TryRecoverLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt);
+  Status TryCheckinLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt);
+  /*!
+   * \brief two-pass message passing over the tree: out[i] = func(node, in[others], i) is sent
+   *        on link i, in[i] is what link i sent (reference allreduce_robust-inl.h:33-166)
+   */
+  template <typename NodeT, typename EdgeT>
+  Status MsgPassing(const NodeT &node, std::vector<EdgeT> *p_in, std::vector<EdgeT> *p_out,
+                    EdgeT (*func)(const NodeT &, const std::vector<EdgeT> &, size_t));
+  void LocalModelCheck(bool with_local);
+
+  // ---- bootstrap cache (ops issued before LoadCheckPoint)
+  int SetBootstrapCache(const std::string &key, const void *buf, size_t nbytes);
+  int GetBootstrapCache(const std::string &key, void *buf, size_t nbytes);
+
+  // ---- watchdog
+  void WatchdogLoop();
+  void StartWatchdog();
+  void StopWatchdog();
+
+  // parameters
+  int num_global_replica_{5};
+  int num_local_replica_{0};
+  int default_local_replica_{2};
+  bool elide_consensus_{true};
+  // state
+  int result_buffer_round_{1};
+  int cur_cache_seq_{0};
+  int local_chkpt_version_{0};
+  int use_local_model_{-1};
+  int recover_counter_{0};
+  bool checkpoint_loaded_{false};
+  bool fast_mode_{false};
+  ResultLog resbuf_, cachebuf_, lookupbuf_;
+  std::string global_checkpoint_;
+  const Serializable *global_lazycheck_{nullptr};
+  std::vector<size_t> local_rptr_[2];
+  std::string local_chkpt_[2];
+  // watchdog
+  TimeoutHandler timeout_handler_{nullptr};
+  std::thread watchdog_;
+  std::mutex wd_mu_;
+  std::condition_variable wd_cv_;
+  bool wd_stop_{false};
+  std::atomic<double> recovering_since_{0.0};
+  std::atomic<bool> watchdog_fired_{false};
+};
+}  // namespace engine
+}  // namespace rabit
+#endif  // XRABIT_ENGINE_ENGINE_ROBUST_H_

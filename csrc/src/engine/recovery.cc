@@ -1,0 +1,644 @@
+/*!
+ * \file recovery.cc
+ * \brief Recovery protocol of the robust engine.
+ *
+ * Parity: reference `src/allreduce_robust.cc:687-1587` and `src/allreduce_robust-inl.h`.
+ *  - RecoverExec: consensus loop deciding, from the reduced ActionSummary, whether to serve a
+ *    checkpoint load, replay a result to a lagging peer, restore bootstrap-cache entries, or
+ *    execute the requested action;
+ *  - TryDecideRouting: two tree message-passing rounds (nearest holder by hop count, then the
+ *    set of edges that must carry data) -> TryRecoverData streams the bytes along that route,
+ *    relaying through bounded staging rings on pass-through nodes;
+ *  - local (per-rank) checkpoints are replicated to the next num_local_replica ring successors
+ *    and recovered with one backward and one forward ring pass.
+ * HBM-resident results are staged through host memory only on ranks that are on the route.
+ */
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <utility>
+
+#include "engine/engine_robust.h"
+#include "rabit/internal/io.h"
+#include "rabit/internal/timer.h"
+#include "rabit/internal/utils.h"
+
+namespace rabit {
+namespace engine {
+
+// ------------------------------------------------------------------ failure handling
+bool EngineRobust::CheckAndRecover(Status s) {
+  if (s == Status::kSuccess) {
+    recovering_since_.store(0.0);
+    return true;
+  }
+  const double t0 = utils::GetTime();
+  fast_mode_ = false;
+  recover_counter_ += 1;
+  stats_.n_recover_events += 1;
+  if (recovering_since_.load() == 0.0) recovering_since_.store(t0);
+  if (debug_) {
+    utils::HandleLogInfo("[%d] failure detected (%s, link %d), recovering\n", rank_,
+                         net::StatusName(s),
+                         host_->err_link() != nullptr ? host_->err_link()->rank : -1);
+  }
+  // the communicator contains the failed peer: abort it, a new epoch is built on demand
+  if (dev_) dev_->AbortComm();
+  // simplest consistent repair: drop every link so the failure propagates, then rejoin
+  for (auto &l : topo_.links) l->sock.Close();
+  // spread the reconnect load on the tracker
+  std::this_thread::sleep_for(std::chrono::milliseconds(10 * std::max(rank_, 0)));
+  ReconnectLinks("recover");
+  stats_.t_recover += utils::GetTime() - t0;
+  return false;
+}
+
+// ------------------------------------------------------------------ message passing
+template <typename NodeT, typename EdgeT>
+Status EngineRobust::MsgPassing(const NodeT &node, std::vector<EdgeT> *p_in,
+                                std::vector<EdgeT> *p_out,
+                                EdgeT (*func)(const NodeT &, const std::vector<EdgeT> &, size_t)) {
+  auto &links = topo_.tree;
+  const int nlink = static_cast<int>(links.size());
+  const int pidx = topo_.parent_index;
+  std::vector<EdgeT> &in = *p_in;
+  std::vector<EdgeT> &out = *p_out;
+  in.assign(nlink, EdgeT());
+  out.assign(nlink, EdgeT());
+  if (nlink == 0) return Status::kSuccess;
+  constexpr size_t kSz = sizeof(EdgeT);
+  std::vector<size_t> nrecv(nlink, 0), nsent(nlink, 0);
+  std::vector<char> ready(nlink, 0);
+  bool up_done = false, down_done = false;
+  net::Poller poller;
+  for (;;) {
+    if (host_->Aborted()) return host_->Fail(nullptr, Status::kAborted);
+    bool children_in = true;
+    for (int i = 0; i < nlink; ++i) {
+      if (i != pidx && nrecv[i] != kSz) children_in = false;
+    }
+    // upward: once every child reported, send the aggregate to the parent
+    if (children_in && !up_done) {
+      if (pidx >= 0) {
+        out[pidx] = func(node, in, static_cast<size_t>(pidx));
+        ready[pidx] = 1;
+      }
+      up_done = true;
+    }
+    // downward: once the parent answered, every child gets its message
+    const bool parent_in = pidx < 0 || nrecv[pidx] == kSz;
+    if (up_done && parent_in && !down_done) {
+      for (int i = 0; i < nlink; ++i) {
+        if (i == pidx) continue;
+        out[i] = func(node, in, static_cast<size_t>(i));
+        ready[i] = 1;
+      }
+      down_done = true;
+    }
+    bool done = down_done;
+    poller.Clear();
+    for (int i = 0; i < nlink; ++i) {
+      if (nrecv[i] != kSz) {
+        done = false;
+        poller.WatchRead(links[i]->sock.fd());
+      }
+      if (nsent[i] != kSz) {
+        done = false;
+        if (ready[i]) poller.WatchWrite(links[i]->sock.fd());
+      }
+    }
+    if (done) break;
+    if (poller.Poll(host_->poll_ms()) == 0) continue;
+    for (int i = 0; i < nlink; ++i) {
+      const int fd = links[i]->sock.fd();
+      if (nrecv[i] != kSz && poller.CanRead(fd)) {
+        ssize_t k = links[i]->sock.Recv(reinterpret_cast<char *>(&in[i]) + nrecv[i],
+                                        kSz - nrecv[i]);
+        if (k > 0) {
+          nrecv[i] += static_cast<size_t>(k);
+        } else {
+          Status st = k == 0 ? Status::kRecvZeroLen : net::StatusFromErrno();
+          if (st != Status::kSuccess) return host_->Fail(links[i], st);
+        }
+      }
+      if (ready[i] && nsent[i] != kSz && poller.CanWrite(fd)) {
+        ssize_t k = links[i]->sock.Send(reinterpret_cast<const char *>(&out[i]) + nsent[i],
+                                        kSz - nsent[i]);
+        if (k >= 0) {
+          nsent[i] += static_cast<size_t>(k);
+        } else {
+          Status st = net::StatusFromErrno();
+          if (st != Status::kSuccess) return host_->Fail(links[i], st);
+        }
+      }
+    }
+  }
+  return Status::kSuccess;
+}
+
+namespace {
+/*! \brief (hops to the nearest data holder, data size) seen through an edge */
+typedef std::pair<int, size_t> DistMsg;
+constexpr int kUnreachable = std::numeric_limits<int>::max();
+
+DistMsg ShortestDist(const std::pair<bool, size_t> &node, const std::vector<DistMsg> &in,
+                     size_t out_index) {
+  if (node.first) return DistMsg(1, node.second);
+  DistMsg best(kUnreachable, 0);
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (i == out_index || in[i].first == kUnreachable) continue;
+    if (in[i].first + 1 < best.first) best = DistMsg(in[i].first + 1, in[i].second);
+  }
+  return best;
+}
+
+/*! \brief 1 if data must flow to us over out_index (we or someone behind us requests it) */
+char DataRequest(const std::pair<bool, int> &node, const std::vector<char> &in,
+                 size_t out_index) {
+  if (static_cast<int>(out_index) != node.second) return 0;
+  if (node.first) return 1;
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (i != out_index && in[i] != 0) return 1;
+  }
+  return 0;
+}
+}  // namespace
+
+Status EngineRobust::TryDecideRouting(RecoverType role, size_t *p_size, int *p_recvlink,
+                                      std::vector<bool> *p_req_in) {
+  int best_link = -2;
+  {
+    std::vector<DistMsg> dist_in, dist_out;
+    Status s = MsgPassing(std::make_pair(role == kHaveData, *p_size), &dist_in, &dist_out,
+                          ShortestDist);
+    if (s != Status::kSuccess) return s;
+    if (role != kHaveData) {
+      for (size_t i = 0; i < dist_in.size(); ++i) {
+        if (dist_in[i].first == kUnreachable) continue;
+        utils::Check(best_link == -2 || *p_size == dist_in[i].second,
+                     "[%d] recovery: inconsistent data size (%zu vs %zu)", rank_, *p_size,
+                     dist_in[i].second);
+        if (best_link == -2 || dist_in[i].first < dist_in[best_link].first) {
+          best_link = static_cast<int>(i);
+          *p_size = dist_in[i].second;
+        }
+      }
+      utils::Check(best_link != -2, "Too many nodes went down and we cannot recover..");
+    } else {
+      best_link = -1;
+    }
+  }
+  std::vector<char> req_in, req_out;
+  Status s = MsgPassing(std::make_pair(role == kRequestData, best_link), &req_in, &req_out,
+                        DataRequest);
+  if (s != Status::kSuccess) return s;
+  p_req_in->assign(req_in.size(), false);
+  for (size_t i = 0; i < req_in.size(); ++i) {
+    (*p_req_in)[i] = req_in[i] != 0;
+    if (req_out[i] != 0) {
+      utils::Assert(req_in[i] == 0, "cannot both request and serve on one link");
+      utils::Assert(static_cast<int>(i) == best_link, "request routed off the best link");
+    }
+  }
+  *p_recvlink = best_link;
+  return Status::kSuccess;
+}
+
+Status EngineRobust::TryRecoverData(RecoverType role, void *buf_, size_t size, int recv_link,
+                                    const std::vector<bool> &req_in) {
+  auto &links = topo_.tree;
+  const int nlink = static_cast<int>(links.size());
+  if (nlink == 0 || size == 0) return Status::kSuccess;
+  utils::Assert(static_cast<int>(req_in.size()) == nlink, "TryRecoverData: request vector");
+  bool involved = role == kRequestData;
+  for (int i = 0; i < nlink; ++i) {
+    if (req_in[i]) {
+      utils::Assert(i != recv_link, "TryRecoverData: serving the link we receive from");
+      involved = true;
+    }
+  }
+  if (!involved) return Status::kSuccess;
+  utils::Assert(recv_link >= 0 || role == kHaveData, "TryRecoverData: no receive link");
+  char *buf = static_cast<char *>(buf_);
+  net::PeerLink *src = recv_link >= 0 ? links[recv_link] : nullptr;
+  if (role == kPassData) src->InitRing(1, size, hcfg_.reduce_buffer_bytes);
+  for (auto *l : links) l->ResetProgress();
+  net::Poller poller;
+  for (;;) {
+    if (host_->Aborted()) return host_->Fail(nullptr, Status::kAborted);
+    // bytes this node can forward so far
+    const size_t avail = role == kHaveData ? size : src->size_read;
+    bool done = true;
+    poller.Clear();
+    if (src != nullptr && src->size_read != size) {
+      done = false;
+      poller.WatchRead(src->sock.fd());
+    }
+    for (int i = 0; i < nlink; ++i) {
+      if (!req_in[i] || links[i]->size_write == size) continue;
+      done = false;
+      if (links[i]->size_write < avail) poller.WatchWrite(links[i]->sock.fd());
+    }
+    if (done) break;
+    if (poller.Poll(host_->poll_ms()) == 0) continue;
+    if (src != nullptr && src->size_read != size && poller.CanRead(src->sock.fd())) {
+      Status s;
+      if (role == kRequestData) {
+        s = src->RecvTo(buf, size);
+      } else {
+        // relay: never overwrite bytes some requester has not received yet
+        size_t min_write = size;
+        for (int i = 0; i < nlink; ++i) {
+          if (req_in[i]) min_write = std::min(min_write, links[i]->size_write);
+        }
+        s = src->FillRing(min_write, size);
+      }
+      if (s != Status::kSuccess) return host_->Fail(src, s);
+    }
+    const size_t avail2 = role == kHaveData ? size : src->size_read;
+    for (int i = 0; i < nlink; ++i) {
+      net::PeerLink *l = links[i];
+      if (!req_in[i] || l->size_write >= avail2 || !poller.CanWrite(l->sock.fd())) continue;
+      if (role == kPassData) {
+        const size_t cap = src->ring_bytes();
+        const size_t off = l->size_write % cap;
+        const size_t len = std::min(cap - off, avail2 - l->size_write);
+        ssize_t k = l->sock.Send(src->ring() + off, len);
+        if (k >= 0) {
+          l->size_write += static_cast<size_t>(k);
+        } else {
+          Status st = net::StatusFromErrno();
+          if (st != Status::kSuccess) return host_->Fail(l, st);
+        }
+      } else {
+        Status st = l->SendFrom(buf, avail2);
+        if (st != Status::kSuccess) return host_->Fail(l, st);
+      }
+    }
+  }
+  return Status::kSuccess;
+}
+
+// ------------------------------------------------------------------ results & checkpoints
+Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, bool requester) {
+  if (static_cast<uint32_t>(seqno) == ActionSummary::kLocalCheckAck) return Status::kSuccess;
+  if (static_cast<uint32_t>(seqno) == ActionSummary::kLocalCheckPoint) {
+    const int nv = !local_chkpt_version_;
+    const int nlocal = std::max(static_cast<int>(local_rptr_[nv].size()) - 1, 0);
+    utils::Assert(nlocal == 1 || nlocal == num_local_replica_ + 1,
+                  "TryGetResult: local checkpoint state");
+    return TryRecoverLocalState(&local_rptr_[nv], &local_chkpt_[nv]);
+  }
+  RecoverType role;
+  void *data = nullptr;
+  bool data_dev = false;
+  if (!requester) {
+    const ResultLog::Entry *e = resbuf_.Query(seqno);
+    if (e != nullptr) {
+      role = kHaveData;
+      size = e->size;
+      data = resbuf_.Data(*e);
+      data_dev = e->on_device;
+    } else {
+      role = kPassData;
+    }
+  } else {
+    role = kRequestData;
+    data = sendrecvbuf;
+    data_dev = OnDevice(sendrecvbuf);
+  }
+  int recv_link;
+  std::vector<bool> req_in;
+  size_t data_size = size;
+  Status s = TryDecideRouting(role, &data_size, &recv_link, &req_in);
+  if (s != Status::kSuccess) return s;
+  utils::Check(data_size != 0, "zero size check point is not allowed");
+  if (role == kRequestData || role == kHaveData) {
+    utils::Check(data_size == size,
+                 "Allreduce recovered data size does not match the call (%zu vs %zu). Check "
+                 "that the recovered program issues the same calls in this version",
+                 data_size, size);
+  }
+  if (data_dev) {
+    // HBM-resident: stage through host memory, only if this rank is on the route
+    const bool on_route = role == kRequestData ||
+                          std::find(req_in.begin(), req_in.end(), true) != req_in.end();
+    if (!on_route) return Status::kSuccess;
+    std::vector<uint64_t> tmp((data_size + 7) / 8);
+    if (role == kHaveData) dev_->StageToHost(tmp.data(), data, data_size);
+    s = TryRecoverData(role, tmp.data(), data_size, recv_link, req_in);
+    if (s == Status::kSuccess && role == kRequestData) {
+      dev_->EnterFromUser();
+      dev_->StageToDevice(data, tmp.data(), data_size);
+      dev_->Finish(MakeProbe(), false);
+    }
+    return s;
+  }
+  return TryRecoverData(role, data, data_size, recv_link, req_in);
+}
+
+Status EngineRobust::TryLoadCheckPoint(bool requester) {
+  const RecoverType role = requester ? kRequestData : kHaveData;
+  Status s;
+  if (num_local_replica_ != 0) {
+    if (requester) {
+      local_rptr_[local_chkpt_version_].clear();
+      local_chkpt_[local_chkpt_version_].clear();
+    }
+    s = TryRecoverLocalState(&local_rptr_[local_chkpt_version_],
+                             &local_chkpt_[local_chkpt_version_]);
+    if (s != Status::kSuccess) return s;
+    const int nlocal =
+        std::max(static_cast<int>(local_rptr_[local_chkpt_version_].size()) - 1, 0);
+    // 1: complete, 2: nothing, 4: partial; any partial node fails the load
+    unsigned state = nlocal == num_local_replica_ + 1 ? 1u : (nlocal == 0 ? 2u : 4u);
+    s = host_->TreeAllreduce(&state, sizeof(state), 1,
+                             coll::HostReducer(mpi::kUInt, mpi::kBitwiseOR));
+    if (s != Status::kSuccess) return s;
+    utils::Check(state == 1 || state == 2,
+                 "LoadCheckPoint: too many nodes failed, cannot recover local state");
+  }
+  if (role == kHaveData && global_lazycheck_ != nullptr) {
+    // materialise a lazy checkpoint now that a peer needs the bytes
+    global_checkpoint_.clear();
+    utils::MemoryBufferStream fs(&global_checkpoint_);
+    fs.Write(&version_number_, sizeof(version_number_));
+    global_lazycheck_->Save(&fs);
+    global_lazycheck_ = nullptr;
+  }
+  size_t size = global_checkpoint_.length();
+  int recv_link;
+  std::vector<bool> req_in;
+  s = TryDecideRouting(role, &size, &recv_link, &req_in);
+  if (s != Status::kSuccess) return s;
+  if (role == kRequestData) global_checkpoint_.resize(size);
+  if (size == 0) return Status::kSuccess;
+  return TryRecoverData(role, BeginPtr(global_checkpoint_), size, recv_link, req_in);
+}
+
+Status EngineRobust::TryRestoreCache(bool requester, int min_seq, int max_seq) {
+  (void)min_seq;
+  if (requester) {
+    utils::Assert(cur_cache_seq_ <= max_seq, "requester should hold fewer cache entries");
+    cachebuf_.Clear();
+    lookupbuf_.Clear();
+    cur_cache_seq_ = 0;
+  }
+  const RecoverType role = requester ? kRequestData : kHaveData;
+  size_t size = 1;
+  int recv_link;
+  std::vector<bool> req_in;
+  Status s = TryDecideRouting(role, &size, &recv_link, &req_in);
+  if (s != Status::kSuccess) return s;
+  for (int i = 0; i < max_seq; ++i) {
+    for (ResultLog *log : {&lookupbuf_, &cachebuf_}) {
+      uint64_t nbytes = 0;
+      if (!requester) {
+        const ResultLog::Entry *e = log->Query(i);
+        utils::Assert(e != nullptr, "bootstrap cache entry %d missing on a holder", i);
+        nbytes = e->size;
+      }
+      s = TryRecoverData(role, &nbytes, sizeof(nbytes), recv_link, req_in);
+      if (s != Status::kSuccess) return s;
+      void *data;
+      if (requester) {
+        log->AllocTemp(nbytes, false);
+        log->PushTemp(i, nbytes);
+        data = log->Data(*log->Query(i));
+      } else {
+        data = log->Data(*log->Query(i));
+      }
+      s = TryRecoverData(role, data, nbytes, recv_link, req_in);
+      if (s != Status::kSuccess) return s;
+    }
+    if (requester) cur_cache_seq_ += 1;
+  }
+  return Status::kSuccess;
+}
+
+// ------------------------------------------------------------------ local state on the ring
+Status EngineRobust::TryRecoverLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt) {
+  if (num_local_replica_ == 0) return Status::kSuccess;
+  std::vector<size_t> &rptr = *p_rptr;
+  std::string &chkpt = *p_chkpt;
+  if (rptr.empty()) {
+    rptr.push_back(0);
+    utils::Assert(chkpt.empty(), "local checkpoint storage inconsistent");
+  }
+  const int n = num_local_replica_;
+  net::PeerLink *next = topo_.ring_next, *prev = topo_.ring_prev;
+  // Slot k of a node holds the local model of the node k hops back on the ring
+  // (slot 0 = own).  Backward pass (next -> prev): a node refills its low slots from its
+  // successors, which hold its model one slot further.  Forward pass (prev -> next): it then
+  // refills the remaining high slots from its predecessor.
+  {
+    const int nlocal = static_cast<int>(rptr.size()) - 1;
+    utils::Assert(nlocal <= n + 1, "too many local replicas");
+    std::vector<int> msg_back(n + 1);
+    msg_back[0] = nlocal;  // -> msg_back[i] = slot count of the i-th successor
+    Status s = host_->RingPass(msg_back.data(), sizeof(int), (n + 1) * sizeof(int), 0,
+                               n * sizeof(int), next, prev);
+    if (s != Status::kSuccess) return s;
+    int msg_fwd[2] = {nlocal, 0};  // -> msg_fwd[1] = slot count of the predecessor
+    s = host_->RingPass(msg_fwd, sizeof(int), 2 * sizeof(int), 0, sizeof(int), prev, next);
+    if (s != Status::kSuccess) return s;
+    int nread_end = nlocal;
+    for (int i = 1; i <= n; ++i) nread_end = std::max(nread_end, msg_back[i] - i);
+    const int nwrite_start = std::min(msg_fwd[1] + 1, nread_end);
+    std::vector<size_t> sizes(nread_end);
+    for (int i = 0; i < nlocal; ++i) sizes[i] = rptr[i + 1] - rptr[i];
+    s = host_->RingPass(sizes.data(), nlocal * sizeof(size_t), nread_end * sizeof(size_t),
+                        nwrite_start * sizeof(size_t), nread_end * sizeof(size_t), next, prev);
+    if (s != Status::kSuccess) return s;
+    rptr.resize(nread_end + 1);
+    for (int i = nlocal; i < nread_end; ++i) rptr[i + 1] = rptr[i] + sizes[i];
+    chkpt.resize(rptr.back());
+    s = host_->RingPass(BeginPtr(chkpt), rptr[nlocal], rptr[nread_end], rptr[nwrite_start],
+                        rptr[nread_end], next, prev);
+    if (s != Status::kSuccess) {
+      rptr.resize(nlocal + 1);
+      chkpt.resize(rptr.back());
+      return s;
+    }
+  }
+  {
+    const int nlocal = static_cast<int>(rptr.size()) - 1;
+    utils::Assert(nlocal <= n + 1, "too many local replicas");
+    std::vector<int> msg_fwd(n + 1);
+    msg_fwd[0] = nlocal;  // -> msg_fwd[i] = slot count of the i-th predecessor
+    Status s = host_->RingPass(msg_fwd.data(), sizeof(int), (n + 1) * sizeof(int), 0,
+                               n * sizeof(int), prev, next);
+    if (s != Status::kSuccess) return s;
+    int msg_back[2] = {nlocal, 0};  // -> msg_back[1] = slot count of the successor
+    s = host_->RingPass(msg_back, sizeof(int), 2 * sizeof(int), 0, sizeof(int), next, prev);
+    if (s != Status::kSuccess) return s;
+    int nread_end = nlocal, nwrite_end = 1;
+    if (nlocal != 0) {
+      // slot i arrives from the predecessor chain as long as every hop up to i holds data
+      for (int i = 1; i <= n; ++i) {
+        if (msg_fwd[i] == 0) break;
+        nread_end = std::max(nread_end, i + 1);
+        nwrite_end = i + 1;
+      }
+      if (nwrite_end > n) nwrite_end = n;
+    } else {
+      nread_end = 0;
+      nwrite_end = 0;
+    }
+    int nwrite_start = std::min(msg_back[1] - 1, nwrite_end);
+    if (nwrite_start < 0) nwrite_start = nwrite_end = 0;  // successor lost its own state
+    std::vector<size_t> sizes(nread_end);
+    for (int i = 0; i < nlocal; ++i) sizes[i] = rptr[i + 1] - rptr[i];
+    s = host_->RingPass(sizes.data(), nlocal * sizeof(size_t), nread_end * sizeof(size_t),
+                        nwrite_start * sizeof(size_t), nwrite_end * sizeof(size_t), prev, next);
+    if (s != Status::kSuccess) return s;
+    rptr.resize(nread_end + 1);
+    for (int i = nlocal; i < nread_end; ++i) rptr[i + 1] = rptr[i] + sizes[i];
+    chkpt.resize(rptr.back());
+    s = host_->RingPass(BeginPtr(chkpt), rptr[nlocal], rptr[nread_end], rptr[nwrite_start],
+                        rptr[nwrite_end], prev, next);
+    if (s != Status::kSuccess) {
+      rptr.resize(nlocal + 1);
+      chkpt.resize(rptr.back());
+      return s;
+    }
+  }
+  return Status::kSuccess;
+}
+
+Status EngineRobust::TryCheckinLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt) {
+  if (num_local_replica_ == 0) return Status::kSuccess;
+  std::vector<size_t> &rptr = *p_rptr;
+  std::string &chkpt = *p_chkpt;
+  utils::Assert(rptr.size() == 2, "TryCheckinLocalState needs exactly the own state");
+  const int n = num_local_replica_;
+  net::PeerLink *next = topo_.ring_next, *prev = topo_.ring_prev;
+  std::vector<size_t> sizes(n + 1);
+  sizes[0] = rptr[1] - rptr[0];
+  Status s = host_->RingPass(sizes.data(), sizeof(size_t), (n + 1) * sizeof(size_t), 0,
+                             n * sizeof(size_t), prev, next);
+  if (s != Status::kSuccess) return s;
+  rptr.resize(n + 2);
+  for (int i = 1; i <= n; ++i) rptr[i + 1] = rptr[i] + sizes[i];
+  chkpt.resize(rptr.back());
+  s = host_->RingPass(BeginPtr(chkpt), rptr[1], rptr[n + 1], rptr[0], rptr[n], prev, next);
+  if (s != Status::kSuccess) {
+    rptr.resize(2);
+    chkpt.resize(rptr.back());
+  }
+  return s;
+}
+
+// ------------------------------------------------------------------ consensus state machine
+bool EngineRobust::RecoverExec(void *buf, size_t size, int flag, int seqno, int cache_seqno,
+                               const char *caller) {
+  if (flag != 0 && flag != ActionSummary::kLoadBootstrapCache) {
+    utils::Assert(static_cast<uint32_t>(seqno) == ActionSummary::kSpecialOp,
+                  "%s: only normal operations carry a sequence number", caller);
+  }
+  utils::Assert(seqno >= 0, "%s: negative seqno %d (flag %d, version %d)", caller, seqno, flag,
+                version_number_);
+  // steady state: everybody agreed to execute the previous op and nobody saw a failure
+  // since, so the only possible outcome of this round is "execute"
+  if (fast_mode_ && flag == 0 && static_cast<uint32_t>(seqno) < ActionSummary::kLocalCheckPoint) {
+    stats_.n_consensus_elided += 1;
+    return false;
+  }
+  const ActionSummary req(flag, flag, static_cast<uint32_t>(seqno),
+                          static_cast<uint32_t>(cache_seqno));
+  for (;;) {
+    ReportStatus();
+    ActionSummary act = req;
+    const double t0 = utils::GetTime();
+    Status s = host_->TreeAllreduce(&act, sizeof(act), 1, ActionSummary::Reducer);
+    stats_.n_consensus += 1;
+    stats_.t_consensus += utils::GetTime() - t0;
+    if (!CheckAndRecover(s)) continue;
+
+    if (act.check_ack()) {
+      if (act.check_point()) {
+        utils::Assert(!act.diff_seq(), "check ack & check pt cannot mix with normal ops");
+        if (req.check_point()) return true;
+      } else if (act.load_check()) {
+        if (!CheckAndRecover(TryLoadCheckPoint(req.load_check()))) continue;
+        if (req.load_check()) return true;
+      } else if (req.check_ack()) {
+        return true;
+      }
+      continue;  // the requested action is not done yet
+    }
+    if (act.check_point()) {
+      if (act.diff_seq()) {
+        // some nodes reached the checkpoint, others lag behind: the laggards (min seqno)
+        // replay from the result log
+        utils::Assert(act.seqno() != ActionSummary::kSpecialOp, "min seq bug");
+        if (debug_) {
+          utils::HandleLogInfo("[%d] %s: checkpoint with lagging peers (min seq %u)\n", rank_,
+                               caller, act.seqno());
+        }
+        const bool requester = req.seqno() == act.seqno();
+        if (!act.load_cache()) {
+          if (act.seqno() > 0) {
+            if (!requester) utils::Assert(req.check_point(), "checkpointing node must hold data");
+            if (!CheckAndRecover(TryGetResult(buf, size, static_cast<int>(act.seqno()),
+                                              requester))) {
+              continue;
+            }
+          }
+        } else {
+          utils::Assert(act.seqno(kCache) != ActionSummary::kSpecialOp, "checkpoint cache seq");
+          int max_cache_seq = cur_cache_seq_;
+          if (host_->TreeAllreduce(&max_cache_seq, sizeof(max_cache_seq), 1,
+                                   coll::HostReducer(mpi::kInt, mpi::kMax)) != Status::kSuccess) {
+            continue;
+          }
+          if (TryRestoreCache(req.load_cache(), static_cast<int>(act.seqno()), max_cache_seq) !=
+              Status::kSuccess) {
+            continue;
+          }
+        }
+        if (requester) return true;
+      } else if (req.check_point()) {
+        return true;
+      }
+      continue;
+    }
+    if (act.load_check()) {
+      // every node asked to load: fresh start, nothing to recover
+      if (!act.diff_seq()) return false;
+      if (!CheckAndRecover(TryLoadCheckPoint(req.load_check()))) continue;
+      if (req.load_check()) return true;
+      continue;
+    }
+    if (act.load_cache()) {
+      utils::Assert(!act.check_point() && !act.check_ack(),
+                    "bootstrap cache restore cannot overlap a checkpoint");
+      if (act.load_cache(kCache)) return false;  // everybody is a requester: nothing cached
+      if (act.diff_seq()) {
+        if (TryRestoreCache(req.load_cache(), static_cast<int>(act.seqno()),
+                            static_cast<int>(act.seqno(kCache))) != Status::kSuccess) {
+          continue;
+        }
+      }
+      if (req.load_cache()) return true;
+      continue;
+    }
+    utils::Assert(!req.load_cache(), "load cache request reached sequence catch-up");
+    utils::Assert(act.seqno() != ActionSummary::kSpecialOp, "min seq bug");
+    if (act.diff_seq()) {
+      const bool requester = req.seqno() == act.seqno();
+      if (!CheckAndRecover(TryGetResult(buf, size, static_cast<int>(act.seqno()), requester))) {
+        continue;
+      }
+      if (requester) return true;
+      continue;
+    }
+    // every node proposes the same newest action: execute it
+    if (elide_consensus_ && !bootstrap_cache_ && flag == 0) fast_mode_ = true;
+    return false;
+  }
+}
+}  // namespace engine
+}  // namespace rabit

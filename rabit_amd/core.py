@@ -1,0 +1,352 @@
+"""Python API of xrabit.
+
+Drop-in for the reference binding (`python/rabit.py:83-364`): init, finalize, get_rank,
+get_world_size, tracker_print, get_processor_name, broadcast (pickled objects), allreduce
+(numpy), load_checkpoint, checkpoint, version_number, with the MAX/MIN/SUM/BITOR constants.
+
+MI355X extensions: `allreduce` also takes torch tensors; HBM (CUDA/HIP) tensors are reduced
+in place over RCCL/xGMI and the CDNA4 kernels, ordered on torch's current stream.  Plus
+`allgather`, `broadcast_tensor`, `allreduce_prepared` (fused lazy prepare), `lazy_checkpoint`,
+`stats`, `engine_name`, `get_device`.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import pickle
+import sys
+from typing import Any, Callable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+MAX = 0
+MIN = 1
+SUM = 2
+BITOR = 3
+
+# prepare ops of allreduce_prepared (csrc/src/device/kernels.h)
+PREP_COPY = 0
+PREP_SQUARE = 1
+PREP_SCALE = 2
+PREP_ABS = 3
+
+_LIB: Optional[ctypes.CDLL] = None
+_LIB_NAME: Optional[str] = None
+
+# numpy dtype -> rabit dtype enum (engine.h mpi::DataType)
+DTYPE_ENUM = {
+    np.dtype("int8"): 0,
+    np.dtype("uint8"): 1,
+    np.dtype("int32"): 2,
+    np.dtype("uint32"): 3,
+    np.dtype("int64"): 4,
+    np.dtype("uint64"): 5,
+    np.dtype("float32"): 6,
+    np.dtype("float64"): 7,
+}
+DTYPE_ENUM__ = DTYPE_ENUM  # reference spelling
+
+
+def _torch_dtype_enum(t) -> int:
+    import torch
+
+    table = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float32: 6,
+             torch.float64: 7}
+    for name, code in (("uint32", 3), ("uint64", 5)):
+        if hasattr(torch, name):
+            table[getattr(torch, name)] = code
+    if t.dtype not in table:
+        raise TypeError("dtype %s is not supported by rabit allreduce" % t.dtype)
+    return table[t.dtype]
+
+
+def _check_init():
+    if _LIB is None:
+        raise RuntimeError("rabit_amd.init() must be called first")
+
+
+def _loadlib(lib: str = "standard", lib_dll=None):
+    global _LIB, _LIB_NAME
+    if lib_dll is not None:
+        _lib._declare(lib_dll)
+        _LIB, _LIB_NAME = lib_dll, "custom"
+        return
+    if _LIB is not None and _LIB_NAME == lib:
+        return
+    _LIB = _lib.load(lib)
+    _LIB_NAME = lib
+
+
+def _unloadlib():
+    global _LIB, _LIB_NAME
+    _LIB, _LIB_NAME = None, None
+
+
+def init(args: Optional[Sequence] = None, lib: str = "standard", lib_dll=None, **params):
+    """Initialise the engine.  `args` are "name=value" strings (e.g. sys.argv); keyword
+    params are appended the same way (init(rabit_debug=1))."""
+    if args is None:
+        args = []
+    args = [a if isinstance(a, bytes) else str(a).encode() for a in args]
+    args += [("%s=%s" % (k, v)).encode() for k, v in params.items()]
+    _loadlib(lib, lib_dll)
+    arr = (ctypes.c_char_p * len(args))(*args)
+    if not _LIB.RabitInit(len(args), arr):
+        raise RuntimeError("rabit init failed: %s" % last_error())
+
+
+def finalize():
+    """Finalize the engine; call after all jobs finished."""
+    if _LIB is None:
+        return
+    _LIB.RabitFinalize()
+    _unloadlib()
+
+
+def get_rank() -> int:
+    _check_init()
+    return _LIB.RabitGetRank()
+
+
+def get_world_size() -> int:
+    _check_init()
+    return _LIB.RabitGetWorldSize()
+
+
+def is_distributed() -> bool:
+    _check_init()
+    return bool(_LIB.RabitIsDistributed())
+
+
+def get_ring_prev_rank() -> int:
+    _check_init()
+    return _LIB.RabitGetRingPrevRank()
+
+
+def tracker_print(msg: Any):
+    """Print a message on the tracker (fixes the reference's c_char_p.encode bug)."""
+    _check_init()
+    if not isinstance(msg, str):
+        msg = str(msg)
+    _LIB.RabitTrackerPrint(msg.encode("utf-8"))
+
+
+def get_processor_name() -> bytes:
+    _check_init()
+    mxlen = 256
+    length = ctypes.c_ulong()
+    buf = ctypes.create_string_buffer(mxlen)
+    _LIB.RabitGetProcessorName(buf, ctypes.byref(length), mxlen)
+    return buf.value
+
+
+def broadcast(data: Any, root: int) -> Any:
+    """Broadcast a picklable object from root; non-roots may pass None."""
+    _check_init()
+    rank = get_rank()
+    length = ctypes.c_ulong()
+    payload = None
+    if root == rank:
+        assert data is not None, "need to pass in data when broadcasting"
+        payload = pickle.dumps(data, protocol=pickle.HIGHEST_PROTOCOL)
+        length.value = len(payload)
+    _LIB.RabitBroadcast(ctypes.byref(length), ctypes.sizeof(ctypes.c_ulong), root)
+    if root != rank:
+        dptr = (ctypes.c_char * length.value)()
+        _LIB.RabitBroadcast(ctypes.cast(dptr, ctypes.c_void_p), length.value, root)
+        data = pickle.loads(dptr.raw)
+    else:
+        buf = ctypes.create_string_buffer(payload, len(payload))
+        _LIB.RabitBroadcast(ctypes.cast(buf, ctypes.c_void_p), length.value, root)
+    return data
+
+
+def _is_torch(x) -> bool:
+    mod = type(x).__module__
+    return mod.startswith("torch") and "torch" in sys.modules and \
+        isinstance(x, sys.modules["torch"].Tensor)
+
+
+def _sync_stream_for(t):
+    """Order device collectives after torch's current stream on t's device."""
+    import torch
+
+    if t.is_cuda:
+        _LIB.RabitSetStream(ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream))
+
+
+def allreduce(data, op: int, prepare_fun: Optional[Callable] = None):
+    """Allreduce.  numpy arrays: returns the reduced array (a flattened copy, as the
+    reference).  torch tensors: reduced in place (must be contiguous) and returned; HBM
+    tensors take the RCCL/HIP path.  prepare_fun(data) runs first unless the result is
+    recovered from peers after a failure."""
+    _check_init()
+    if _is_torch(data):
+        if not data.is_contiguous():
+            raise ValueError("allreduce needs a contiguous tensor")
+        enum = _torch_dtype_enum(data)
+        if data.is_cuda:
+            _sync_stream_for(data)
+        cb = _make_prepare(prepare_fun, data)
+        _LIB.RabitAllreduce(ctypes.c_void_p(data.data_ptr()), data.numel(), enum, op, cb, None)
+        return data
+    if not isinstance(data, np.ndarray):
+        raise TypeError("allreduce only takes numpy.ndarray or torch.Tensor")
+    buf = data.ravel()
+    if buf.base is data.base:
+        buf = buf.copy()
+    if buf.dtype not in DTYPE_ENUM:
+        raise TypeError("data type %s not supported" % str(buf.dtype))
+    if op == BITOR and buf.dtype.kind == "f":
+        raise TypeError("BITOR is not defined for floating point data")
+    cb = _make_prepare(prepare_fun, data)
+    _LIB.RabitAllreduce(buf.ctypes.data_as(ctypes.c_void_p), buf.size, DTYPE_ENUM[buf.dtype], op,
+                        cb, None)
+    return buf
+
+
+def _make_prepare(prepare_fun, data):
+    if prepare_fun is None:
+        return _LIB.PREPARE_FN()
+
+    def pfunc(_arg):
+        prepare_fun(data)
+
+    cb = _LIB.PREPARE_FN(pfunc)
+    _make_prepare.keep = cb  # keep alive for the duration of the call
+    return cb
+
+
+def allreduce_prepared(dst, src, op: int, prep: int = PREP_SQUARE, alpha: float = 1.0):
+    """Fused lazy-prepare allreduce of HBM tensors: dst = prep(src) (gfx950 kernel), then
+    allreduce(dst).  The prepare kernel is skipped when the result is recovered."""
+    _check_init()
+    assert dst.is_cuda and src.is_cuda and dst.numel() == src.numel() and dst.dtype == src.dtype
+    _sync_stream_for(dst)
+    _LIB.RabitDevAllreducePrepared(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                   dst.numel(), _torch_dtype_enum(dst), op, prep, float(alpha))
+    return dst
+
+
+def broadcast_tensor(t, root: int):
+    """In-place broadcast of a contiguous numpy array or torch tensor (host or HBM)."""
+    _check_init()
+    if _is_torch(t):
+        if t.is_cuda:
+            _sync_stream_for(t)
+        _LIB.RabitBroadcast(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(), root)
+        return t
+    assert t.flags["C_CONTIGUOUS"]
+    _LIB.RabitBroadcast(t.ctypes.data_as(ctypes.c_void_p), t.nbytes, root)
+    return t
+
+
+def allgather(data):
+    """Gather equal-size slices from every rank: returns an array of world_size * len(data)
+    (torch tensors stay on their device)."""
+    _check_init()
+    n, r = get_world_size(), get_rank()
+    if _is_torch(data):
+        import torch
+
+        flat = data.contiguous().view(-1)
+        out = torch.empty(n * flat.numel(), dtype=flat.dtype, device=flat.device)
+        out[r * flat.numel():(r + 1) * flat.numel()] = flat
+        if out.is_cuda:
+            _sync_stream_for(out)
+        _LIB.RabitAllgather(ctypes.c_void_p(out.data_ptr()), out.numel(), r * flat.numel(),
+                            flat.numel(), flat.numel(), _torch_dtype_enum(out))
+        return out
+    flat = np.ascontiguousarray(data).ravel()
+    out = np.empty(n * flat.size, dtype=flat.dtype)
+    out[r * flat.size:(r + 1) * flat.size] = flat
+    _LIB.RabitAllgather(out.ctypes.data_as(ctypes.c_void_p), out.size, r * flat.size, flat.size,
+                        flat.size, DTYPE_ENUM[out.dtype])
+    return out
+
+
+def _load_model(ptr, length):
+    data = (ctypes.c_char * length).from_address(ctypes.addressof(ptr.contents))
+    return pickle.loads(data.raw)
+
+
+def load_checkpoint(with_local: bool = False):
+    """Load the latest checkpoint: (version, global[, local]); version 0 means none."""
+    _check_init()
+    gptr = ctypes.POINTER(ctypes.c_char)()
+    glen = ctypes.c_ulong()
+    if with_local:
+        lptr = ctypes.POINTER(ctypes.c_char)()
+        llen = ctypes.c_ulong()
+        version = _LIB.RabitLoadCheckPoint(ctypes.byref(gptr), ctypes.byref(glen),
+                                           ctypes.byref(lptr), ctypes.byref(llen))
+        if version == 0:
+            return (version, None, None)
+        return (version, _load_model(gptr, glen.value), _load_model(lptr, llen.value))
+    version = _LIB.RabitLoadCheckPoint(ctypes.byref(gptr), ctypes.byref(glen), None, None)
+    if version == 0:
+        return (version, None)
+    return (version, _load_model(gptr, glen.value))
+
+
+def checkpoint(global_model: Any, local_model: Any = None):
+    """Checkpoint (pickled) models; the version number increases by one."""
+    _check_init()
+    sglobal = pickle.dumps(global_model)
+    if local_model is None:
+        _LIB.RabitCheckPoint(sglobal, len(sglobal), None, 0)
+    else:
+        slocal = pickle.dumps(local_model)
+        _LIB.RabitCheckPoint(sglobal, len(sglobal), slocal, len(slocal))
+
+
+_lazy_keep = None
+
+
+def lazy_checkpoint(global_model: Any):
+    """Lazy checkpoint: the pickled bytes are kept and only sent if a peer needs them."""
+    global _lazy_keep
+    _check_init()
+    _lazy_keep = pickle.dumps(global_model)
+    _LIB.RabitLazyCheckPoint(_lazy_keep, len(_lazy_keep))
+
+
+def version_number() -> int:
+    _check_init()
+    return _LIB.RabitVersionNumber()
+
+
+# ----------------------------------------------------------------------------- extensions
+def engine_name() -> str:
+    _check_init()
+    return _LIB.RabitEngineName().decode()
+
+
+def get_device() -> int:
+    _check_init()
+    return _LIB.RabitGetDevice()
+
+
+def stats() -> dict:
+    _check_init()
+    return json.loads(_LIB.RabitGetStats().decode())
+
+
+def last_error() -> str:
+    if _LIB is None:
+        return ""
+    return _LIB.RabitGetLastError().decode()
+
+
+def set_error_mode(raise_errors: bool):
+    """raise_errors=False (default): a native error exits the process (the launcher restarts
+    the worker).  True: errors are raised as RuntimeError instead (tests)."""
+    _check_init()
+    _LIB.RabitSetErrorMode(1 if raise_errors else 0)
+
+
+def lib():
+    """The loaded ctypes library (for rabit_amd.ops)."""
+    return _LIB
