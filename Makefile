@@ -69,8 +69,7 @@ $(LIBDIR)/librabit_mock.a: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_mock.o
 	rm -f $@ && ar rcs $@ $^
 
 # ---------------------------------------------------------------- test / example programs
-TEST_PROGS := unit_tests model_recover local_recover lazy_recover speed_test basic \
-              broadcast lazy_allreduce device_selftest
+TEST_PROGS := unit_tests recover_test speed_test basic broadcast lazy_allreduce
 tests: $(foreach p,$(TEST_PROGS),$(BIN)/$(p))
 
 $(BIN)/unit_tests: tests/cpp/unit_tests.cc $(LIBDIR)/librabit_mock.a $(HEADERS)

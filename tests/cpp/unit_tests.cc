@@ -1,0 +1,374 @@
+/*!
+ * \file unit_tests.cc
+ * \brief C++ unit tests (own minimal harness; GoogleTest is not available offline).
+ *
+ * Mirrors the reference's test/cpp suite (test_utils, test_io, allreduce_base_test,
+ * allreduce_mock_test, allreduce_robust_test) against xrabit internals, plus serializer,
+ * reducer and consensus-encoding tests.  All tests run in single-node mode (no tracker).
+ */
+#include <rabit/internal/io.h>
+#include <rabit/internal/utils.h>
+#include <rabit/rabit.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <functional>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "coll/host_coll.h"
+#include "core/params.h"
+#include "engine/engine_mock.h"
+#include "engine/engine_robust.h"
+
+namespace {
+struct TestCase {
+  const char *name;
+  std::function<void()> fn;
+};
+std::vector<TestCase> &Registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+struct Registrar {
+  Registrar(const char *name, std::function<void()> fn) { Registry().push_back({name, fn}); }
+};
+#define TEST(name)                                    \
+  void test_##name();                                 \
+  Registrar reg_##name(#name, test_##name);           \
+  void test_##name()
+
+int g_failures = 0;
+#define EXPECT(cond)                                                              \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      fprintf(stderr, "  EXPECT failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failures;                                                               \
+    }                                                                             \
+  } while (0)
+#define EXPECT_THROW(stmt)            \
+  do {                                \
+    bool thrown = false;              \
+    try {                             \
+      stmt;                           \
+    } catch (const rabit::Error &) {  \
+      thrown = true;                  \
+    }                                 \
+    EXPECT(thrown);                   \
+  } while (0)
+
+std::vector<char *> Argv(std::vector<std::string> &store) {
+  std::vector<char *> v;
+  for (auto &s : store) v.push_back(&s[0]);
+  return v;
+}
+
+// white-box accessors through inheritance (no #define private public)
+class ProbeBase : public rabit::engine::EngineBase {
+ public:
+  const rabit::net::TrackerConfig &tracker() const { return tracker_; }
+  const rabit::coll::HostCollConfig &host() const { return hcfg_; }
+  bool bootstrap() const { return bootstrap_cache_; }
+  bool debug() const { return debug_; }
+  bool timeout() const { return timeout_enabled_; }
+  int timeout_sec() const { return timeout_sec_; }
+};
+
+class ProbeRobust : public rabit::engine::EngineRobust {
+ public:
+  using EngineRobust::ActionSummary;
+  using EngineRobust::ResultLog;
+  static constexpr SeqType kCacheSeq = kCache;
+  int result_round() const { return result_buffer_round_; }
+};
+
+std::atomic<int> g_timeouts{0};
+void CountTimeout(int, int) { g_timeouts.fetch_add(1); }
+}  // namespace
+
+// ---------------------------------------------------------------- utils / io
+TEST(utils_assert_throws) {
+  EXPECT_THROW(rabit::utils::Assert(false, "boom %d", 1));
+  EXPECT_THROW(rabit::utils::Check(false, "bad"));
+  rabit::utils::Assert(true, "never");
+  EXPECT(rabit::utils::StringToBool("true") && rabit::utils::StringToBool("1") &&
+         !rabit::utils::StringToBool("0") && !rabit::utils::StringToBool("false"));
+}
+
+TEST(io_fixed_buffer_seek_end) {
+  std::vector<char> buf(64);
+  rabit::utils::MemoryFixSizeBuffer fs(buf.data(), buf.size());
+  fs.Seek(rabit::utils::MemoryFixSizeBuffer::SeekEnd);
+  EXPECT(fs.Tell() == buf.size());
+  fs.Seek(60);
+  EXPECT_THROW(fs.Write("12345678", 8));
+}
+
+TEST(io_buffer_stream_roundtrip) {
+  std::string blob;
+  rabit::utils::MemoryBufferStream out(&blob);
+  std::vector<float> v = {1.5f, -2.0f, 3.25f};
+  std::string s = "hello";
+  std::vector<std::string> vs = {"a", "", "ccc"};
+  std::map<int, double> m = {{1, 0.5}, {7, 2.0}};
+  int x = 42;
+  out.Write(v);
+  out.Write(s);
+  out.Write(vs);
+  out.Write(m);
+  out.Write(x);
+  // dmlc byte format: uint64 count then payload
+  uint64_t n0;
+  std::memcpy(&n0, blob.data(), 8);
+  EXPECT(n0 == 3 && blob.size() >= 8 + 12);
+  rabit::utils::MemoryBufferStream in(&blob);
+  std::vector<float> v2;
+  std::string s2;
+  std::vector<std::string> vs2;
+  std::map<int, double> m2;
+  int x2 = 0;
+  EXPECT(in.Read(&v2) && in.Read(&s2) && in.Read(&vs2) && in.Read(&m2) && in.Read(&x2));
+  EXPECT(v2 == v && s2 == s && vs2 == vs && m2 == m && x2 == 42);
+  EXPECT(!in.Read(&x2));
+}
+
+TEST(params_parse_unit) {
+  EXPECT(rabit::core::ParseUnit("x", "12") == 12);
+  EXPECT(rabit::core::ParseUnit("x", "3K") == 3u << 10);
+  EXPECT(rabit::core::ParseUnit("x", "256MB") == 256u << 20);
+  EXPECT(rabit::core::ParseUnit("x", "2G") == size_t(2) << 30);
+  EXPECT_THROW(rabit::core::ParseUnit("x", "abc"));
+  EXPECT_THROW(rabit::core::ParseUnit("x", "3Q"));
+}
+
+// ---------------------------------------------------------------- host reducers
+TEST(host_reducers) {
+  using namespace rabit::engine::mpi;
+  std::vector<float> a = {1, 5, 3}, b = {4, 2, 3};
+  rabit::coll::HostReducer(kFloat, kMax)(b.data(), a.data(), 3, MPI::Datatype(4));
+  EXPECT((a == std::vector<float>{4, 5, 3}));
+  std::vector<int64_t> c = {1, 2}, d = {6, 8};
+  rabit::coll::HostReducer(kLongLong, kBitwiseOR)(d.data(), c.data(), 2, MPI::Datatype(8));
+  EXPECT(c[0] == 7 && c[1] == 10);
+  EXPECT(rabit::coll::HostReducer(kDouble, kBitwiseOR) == nullptr);
+  std::vector<unsigned char> e = {200, 3}, f = {100, 9};
+  rabit::coll::HostReducer(kUChar, kMin)(f.data(), e.data(), 2, MPI::Datatype(1));
+  EXPECT(e[0] == 100 && e[1] == 3);
+  EXPECT(rabit::coll::DTypeSize(kChar) == 1 && rabit::coll::DTypeSize(kULong) == 8);
+}
+
+// ---------------------------------------------------------------- base engine params
+TEST(base_params_single_node) {
+  std::vector<std::string> args = {"rabit_task_id=7",      "rabit_bootstrap_cache=1",
+                                   "rabit_debug=true",     "rabit_reduce_ring_mincount=1",
+                                   "rabit_timeout=1",      "rabit_timeout_sec=5",
+                                   "rabit_reduce_buffer=1M", "not_a_param"};
+  auto argv = Argv(args);
+  ProbeBase e;
+  EXPECT(e.Init(static_cast<int>(argv.size()), argv.data()));
+  EXPECT(e.tracker().task_id == "7");
+  EXPECT(e.bootstrap() && e.debug() && e.timeout() && e.timeout_sec() == 5);
+  EXPECT(e.host().reduce_ring_mincount == 1);
+  EXPECT(e.host().reduce_buffer_bytes == (1u << 20));
+  EXPECT(e.GetRank() == 0 && e.GetWorldSize() == 1 && !e.IsDistributed());
+  // single node: collectives return after running prepare
+  int calls = 0;
+  void (*prep)(void *) = [](void *p) { ++*static_cast<int *>(p); };
+  int v = 3;
+  e.Allreduce(&v, 4, 1, rabit::coll::HostReducer(rabit::engine::mpi::kInt, rabit::engine::mpi::kSum),
+              prep, &calls, "f", 1, "c");
+  EXPECT(calls == 1 && v == 3);
+  EXPECT_THROW(ProbeBase().SetParam("rabit_reduce_ring_mincount", "0"));
+  e.Shutdown();
+}
+
+// ---------------------------------------------------------------- mock engine
+TEST(mock_allreduce_throws) {
+  std::vector<std::string> args = {"mock=0,0,0,0"};
+  auto argv = Argv(args);
+  rabit::engine::EngineMock m;
+  m.Init(1, argv.data());
+  m.TestSetState(0, 0, 0);
+  EXPECT_THROW(m.Allreduce(nullptr, 0, 0, nullptr, nullptr, nullptr, "f", 1, "c"));
+}
+
+TEST(mock_broadcast_throws_at_version_seq) {
+  std::vector<std::string> args = {"mock=0,1,2,0"};
+  auto argv = Argv(args);
+  rabit::engine::EngineMock m;
+  m.Init(1, argv.data());
+  m.TestSetState(0, 1, 2);
+  EXPECT_THROW(m.Broadcast(nullptr, 0, 0, "f", 1, "c"));
+  // the trial counter moved on: the same key no longer fires
+  m.Broadcast(nullptr, 0, 0, "f", 1, "c");
+}
+
+TEST(mock_gather_throws) {
+  std::vector<std::string> args = {"mock=0,0,0,0"};
+  auto argv = Argv(args);
+  rabit::engine::EngineMock m;
+  m.Init(1, argv.data());
+  EXPECT_THROW(m.Allgather(nullptr, 0, 0, 0, 0, "f", 1, "c"));
+}
+
+TEST(mock_bad_param) {
+  rabit::engine::EngineMock m;
+  EXPECT_THROW(m.SetParam("mock", "1,2"));
+}
+
+// ---------------------------------------------------------------- robust engine
+TEST(robust_result_round) {
+  std::vector<std::string> args = {"rabit_global_replica=0"};
+  auto argv = Argv(args);
+  ProbeRobust r;
+  r.Init(1, argv.data());
+  EXPECT(r.result_round() == -1);
+  r.Shutdown();
+}
+
+TEST(consensus_reducer) {
+  using AS = ProbeRobust::ActionSummary;
+  AS a(AS::kCheckPoint, 1, 5, 3), b(0, 1, 7, 9);
+  AS::Reducer(&a, &b, 1, MPI::Datatype(8));
+  EXPECT(b.seqno() == 5);
+  EXPECT(b.check_point() && b.diff_seq() && !b.load_check());
+  EXPECT(b.seqno(ProbeRobust::kCacheSeq) == 9);
+  EXPECT(b.flag(ProbeRobust::kCacheSeq) == 1);
+  AS c(AS::kLoadCheck, 0, 4, 2), d(0, 1, 4, 2);
+  AS::Reducer(&c, &d, 1, MPI::Datatype(8));
+  EXPECT(!d.diff_seq() && d.load_check() && d.flag(ProbeRobust::kCacheSeq) == 0);
+}
+
+TEST(result_log_host) {
+  ProbeRobust::ResultLog log;
+  void *p = log.AllocTemp(12, false);
+  std::memcpy(p, "abcdefghijk", 12);
+  log.PushTemp(0, 12);
+  void *q = log.AllocTemp(4, false);
+  std::memcpy(q, "xyz", 4);
+  log.PushTemp(3, 4);
+  EXPECT(log.LastSeqNo() == 3);
+  const auto *e = log.Query(0);
+  EXPECT(e != nullptr && e->size == 12 && !strcmp(static_cast<char *>(log.Data(*e)), "abcdefghijk"));
+  EXPECT(log.Query(1) == nullptr);
+  EXPECT_THROW(log.PushTemp(2, 4));
+  log.DropLast();
+  EXPECT(log.LastSeqNo() == 0);
+  log.Clear();
+  EXPECT(log.LastSeqNo() == -1 && log.size() == 0);
+}
+
+TEST(robust_watchdog_times_out) {
+  std::vector<std::string> args = {"rabit_timeout=1", "rabit_timeout_sec=1"};
+  auto argv = Argv(args);
+  ProbeRobust r;
+  r.SetTimeoutHandler(CountTimeout);
+  r.Init(2, argv.data());
+  g_timeouts = 0;
+  EXPECT(!r.TestCheckAndRecover(rabit::net::Status::kSockError));
+  std::this_thread::sleep_for(std::chrono::milliseconds(1500));
+  EXPECT(g_timeouts.load() == 1 && r.watchdog_fired());
+  r.Shutdown();
+}
+
+TEST(robust_watchdog_recovered_in_time) {
+  std::vector<std::string> args = {"rabit_timeout=1", "rabit_timeout_sec=1"};
+  auto argv = Argv(args);
+  ProbeRobust r;
+  r.SetTimeoutHandler(CountTimeout);
+  r.Init(2, argv.data());
+  g_timeouts = 0;
+  EXPECT(!r.TestCheckAndRecover(rabit::net::Status::kSockError));
+  std::this_thread::sleep_for(std::chrono::milliseconds(400));
+  EXPECT(r.TestCheckAndRecover(rabit::net::Status::kSuccess));
+  std::this_thread::sleep_for(std::chrono::milliseconds(1200));
+  EXPECT(g_timeouts.load() == 0 && !r.watchdog_fired());
+  r.Shutdown();
+}
+
+TEST(robust_watchdog_second_error_keeps_deadline) {
+  std::vector<std::string> args = {"rabit_timeout=1", "rabit_timeout_sec=1", "rabit_debug=1"};
+  auto argv = Argv(args);
+  ProbeRobust r;
+  r.SetTimeoutHandler(CountTimeout);
+  r.Init(3, argv.data());
+  g_timeouts = 0;
+  EXPECT(!r.TestCheckAndRecover(rabit::net::Status::kSockError));
+  std::this_thread::sleep_for(std::chrono::milliseconds(700));
+  EXPECT(!r.TestCheckAndRecover(rabit::net::Status::kConnReset));
+  std::this_thread::sleep_for(std::chrono::milliseconds(600));
+  // 1.3 s after the first error: the deadline counts from the first failure
+  EXPECT(g_timeouts.load() == 1);
+  r.Shutdown();
+}
+
+TEST(robust_shutdown_before_timeout) {
+  std::vector<std::string> args = {"rabit_timeout=1", "rabit_timeout_sec=1"};
+  auto argv = Argv(args);
+  ProbeRobust r;
+  r.SetTimeoutHandler(CountTimeout);
+  r.Init(2, argv.data());
+  g_timeouts = 0;
+  EXPECT(!r.TestCheckAndRecover(rabit::net::Status::kSockError));
+  EXPECT(r.Shutdown());
+  std::this_thread::sleep_for(std::chrono::milliseconds(1200));
+  EXPECT(g_timeouts.load() == 0);
+}
+
+// ---------------------------------------------------------------- public API, single node
+namespace {
+struct Point {
+  double x;
+  int n;
+};
+void AddPoint(Point &dst, const Point &src) {  // NOLINT(*)
+  dst.x += src.x;
+  dst.n += src.n;
+}
+struct Packed {
+  char c[3];
+};
+void MaxPacked(Packed &dst, const Packed &src) {  // NOLINT(*)
+  for (int i = 0; i < 3; ++i) dst.c[i] = std::max(dst.c[i], src.c[i]);
+}
+}  // namespace
+
+TEST(api_uninitialised_single_node) {
+  EXPECT(rabit::GetWorldSize() == 1 && rabit::GetRank() == 0);
+  std::vector<double> v = {1, 2};
+  rabit::Allreduce<rabit::op::Sum>(v.data(), v.size());
+  EXPECT(v[1] == 2);
+  rabit::Reducer<Point, AddPoint> red;
+  Point p[2] = {{1.0, 1}, {2.0, 2}};
+  red.Allreduce(p, 2);
+  EXPECT(p[1].n == 2);
+  rabit::Reducer<Packed, MaxPacked> red2;
+  Packed q[1] = {{{1, 2, 3}}};
+  red2.Allreduce(q, 1, [&]() { q[0].c[0] = 9; });
+  EXPECT(q[0].c[0] == 9);
+  std::string s = "abc";
+  rabit::Broadcast(&s, 0);
+  EXPECT(s == "abc");
+}
+
+int main(int argc, char **argv) {
+  int failed_cases = 0;
+  for (auto &t : Registry()) {
+    if (argc > 1 && std::string(argv[1]) != t.name) continue;
+    const int before = g_failures;
+    try {
+      t.fn();
+    } catch (const std::exception &e) {
+      fprintf(stderr, "  unexpected exception: %s\n", e.what());
+      ++g_failures;
+    }
+    const bool ok = g_failures == before;
+    failed_cases += ok ? 0 : 1;
+    printf("[%s] %s\n", ok ? "  OK  " : " FAIL ", t.name);
+  }
+  printf("%zu tests, %d failed\n", Registry().size(), failed_cases);
+  return failed_cases == 0 ? 0 : 1;
+}

@@ -1,0 +1,75 @@
+"""Multi-process fault-tolerance scenarios on CPU ranks (the reference's test/test.mk matrix).
+
+Each scenario launches 10 worker processes through rabit_amd.launcher (tracker + restarts).
+`mock=rank,version,seqno,trial` kill points make workers die; the launcher restarts them and
+they recover their checkpoint and replay missed collective results from the survivors.
+"""
+import os
+import sys
+
+import pytest
+
+from rabit_amd.launcher import LocalJob
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+DIE = ["mock=0,0,1,0", "mock=1,1,1,0"]
+DIE_SAME = DIE + ["mock=0,1,1,0", "mock=4,1,1,0", "mock=9,1,1,0"]
+DIE_HARD = DIE + ["mock=1,1,1,1", "mock=0,1,1,0", "mock=4,1,1,0", "mock=9,1,1,0",
+                  "mock=8,1,2,0", "mock=4,1,3,0"]
+LOCAL = DIE_SAME + ["mock=1,1,1,1"]
+
+SCENARIOS = {
+    # name: (extra args, expected restarts >= )
+    "model_recover_die": (["mode=global", "rabit_bootstrap_cache=true", "rabit_debug=true",
+                           "rabit_reduce_ring_mincount=1", "rabit_timeout=true",
+                           "rabit_timeout_sec=20"] + DIE, 2),
+    "model_recover_die_same": (["mode=global", "rabit_bootstrap_cache=1"] + DIE_SAME, 3),
+    "model_recover_die_hard": (["mode=global", "rabit_bootstrap_cache=1"] + DIE_HARD, 4),
+    "model_recover_die_hard_elided": (["mode=global"] + DIE_HARD, 4),
+    "model_recover_die_hard_no_elide": (["mode=global", "rabit_elide_consensus=0"] + DIE_HARD, 4),
+    "local_recover": (["mode=local"] + LOCAL, 3),
+    "local_recover_force_local": (["mode=local", "force_local=1"] + LOCAL, 3),
+    "lazy_recover_die_hard": (["mode=lazy"] + DIE_HARD, 4),
+    "lazy_recover_die_same": (["mode=lazy"] + DIE_SAME, 3),
+    "ringallreduce": (["mode=global", "rabit_reduce_ring_mincount=10"], 0),
+    "tree_only_small_buffer": (["mode=global", "rabit_reduce_ring_mincount=100000",
+                                "rabit_reduce_buffer=4K", "rabit_tree_reduce_minsize=1K"] + DIE, 2),
+}
+
+
+def _run(cmd, n=10, attempts=20, timeout=240, env=None):
+    job = LocalJob(cmd, n, attempts, env=env, capture=True, timeout=timeout,
+                   print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    return rc, job, out
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_recover_scenario(native_build, name):
+    args, min_restarts = SCENARIOS[name]
+    rc, job, out = _run([os.path.join(native_build, "recover_test"), "1000"] + args)
+    assert rc == 0, out[-4000:]
+    assert out.count("PASSED") == 10, out[-4000:]
+    restarts = sum(a - 1 for a in job.attempts)
+    assert restarts >= min_restarts, "expected kills did not happen (%d)" % restarts
+
+
+def test_python_local_recover(native_build):
+    """The reference's test/local_recover.py: pickled global + local models under failures."""
+    script = os.path.join(ROOT, "tests", "scripts", "local_recover.py")
+    rc, job, out = _run([sys.executable, script] + LOCAL, timeout=240)
+    assert rc == 0, out[-4000:]
+    assert out.count("DONE") == 10, out[-3000:]
+    assert sum(a - 1 for a in job.attempts) >= 3
+
+
+def test_lazy_prepare_not_rerun_on_replay(native_build):
+    """A restarted worker must not call prepare_fun for results it replays."""
+    script = os.path.join(ROOT, "tests", "scripts", "lazy_prepare.py")
+    rc, job, out = _run([sys.executable, script, "mock=1,0,1,0"], n=4, attempts=3)
+    assert rc == 0, out[-4000:]
+    assert out.count("DONE") == 4
+    # rank 1 died at seq 1 of version 0 and replayed seq 0 without preparing it again
+    assert "[1] replayed-prepare-skipped" in out, out[-3000:]

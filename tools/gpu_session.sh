@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, 1-GPU bench, rocprofv3 kernel profile.
+# Every GPU step has its own time limit; a crash/timeout (rc >= 124) stops the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT="$PWD/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {
+  local name=$1; shift
+  local limit=$1; shift
+  echo "== $name (limit ${limit}s)"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "stopping: $name ended with rc=$rc"; exit $rc
+  fi
+}
+STEPS=${STEPS:-"tests bench prof"}
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof" -o bench -- python3 bench.py --steps 10 --warmup 3 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    speed) step speed 300 python -m rabit_amd.launcher -n 1 -- build/bin/speed_test 33554432 10 device=1 rabit_world1_fastpath=0 ;;
+  esac
+done
+echo "session done"
