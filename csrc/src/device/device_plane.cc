@@ -246,7 +246,8 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
       (void)hipStreamSynchronize(stream_);
       return Status::kTimeout;
     }
-    if (waited * 1e6 > cfg_.spin_us) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // spin first: the wake-up latency after completion sits on the critical path of every op
+    if (waited * 1e6 > cfg_.spin_us) std::this_thread::sleep_for(std::chrono::microseconds(10));
   }
 }
 
@@ -264,6 +265,10 @@ void DevicePlane::Synchronize() { CheckHip(hipStreamSynchronize(stream_), "hipSt
 void DevicePlane::CopyAsync(void *dst, const void *src, size_t bytes) {
   if (bytes == 0 || dst == src) return;
   CheckHip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+}
+
+void DevicePlane::CopyDeviceAsync(void *dst, const void *src, size_t bytes) {
+  CheckHip(LaunchCopy(dst, src, bytes, stream_), "LaunchCopy");
 }
 
 void *DevicePlane::Scratch(size_t bytes, int slot) {
@@ -306,7 +311,7 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
   const size_t tn = TypeBytes(dtype);
   const int n = nranks_;
   if (n == 1) {
-    CopyAsync(recv, send, count * tn);
+    CopyDeviceAsync(recv, send, count * tn);
     return Status::kSuccess;
   }
   // all-to-all: rank k receives everyone's copy of segment k, reduces it with the

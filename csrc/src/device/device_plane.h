@@ -40,7 +40,7 @@ struct DeviceConfig {
   double op_timeout_sec{0};            // 0: no deadline on a device op
   size_t arena_chunk{256u << 20};      // result-log arena growth step
   size_t arena_cap{size_t(64) << 30};  // beyond this the result log falls back to host memory
-  int spin_us{50};                     // busy-poll window before sleeping while waiting
+  int spin_us{5000};                   // busy-poll window before sleeping while waiting
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -107,8 +107,10 @@ class DevicePlane {
   void StageToDevice(void *dev, const void *host, size_t bytes);
 
   // ---- memory / ordering
-  /*! \brief async copy on the plane stream */
+  /*! \brief async copy on the plane stream (any memory kinds) */
   void CopyAsync(void *dst, const void *src, size_t bytes);
+  /*! \brief async HBM-to-HBM copy with the gfx950 copy kernel */
+  void CopyDeviceAsync(void *dst, const void *src, size_t bytes);
   /*! \brief order the plane stream after the user stream */
   void EnterFromUser();
   /*! \brief record completion, order the user stream after it, host-wait if sync */

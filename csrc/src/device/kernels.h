@@ -38,6 +38,9 @@ hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, i
  */
 hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *out,
                           hipStream_t stream);
+/*! \brief device-to-device copy: 16-byte-per-lane kernel for the aligned bulk (the blit
+ *  kernel behind hipMemcpyAsync D2D streams slower), hipMemcpyAsync for an unaligned rest */
+hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stream);
 /*! \brief fill count elements with value (bit pattern of dtype) */
 hipError_t LaunchFill(void *dst, size_t count, int dtype, double value, hipStream_t stream);
 }  // namespace device

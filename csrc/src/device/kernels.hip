@@ -334,6 +334,23 @@ __global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint32_t *__restr
   }
 }
 
+// ---------------------------------------------------------------- copy
+/*! \brief 16-byte-per-lane streaming copy, kUnroll loads in flight per lane */
+__global__ __launch_bounds__(kBlock) void CopyVecKernel(uint4 *__restrict__ dst,
+                                                       const uint4 *__restrict__ src,
+                                                       size_t nvec) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
+    uint4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < nvec; i += stride) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------- fill
 template <typename T>
 __global__ __launch_bounds__(kBlock) void FillKernel(T *dst, size_t n, T value) {
@@ -435,6 +452,24 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
   hipLaunchKernelGGL(ChecksumKernel, dim3(GridFor(nwords / 4 + 1)), dim3(kBlock), 0, stream,
                      static_cast<const uint32_t *>(buf), nwords, out);
   return hipGetLastError();
+}
+
+hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stream) {
+  if (bytes == 0 || dst == src) return hipSuccess;
+  const size_t nvec = Aligned16(dst) && Aligned16(src) ? bytes / 16 : 0;
+  if (nvec != 0) {
+    hipLaunchKernelGGL(CopyVecKernel, dim3(GridFor((nvec + kUnroll - 1) / kUnroll)),
+                       dim3(kBlock), 0, stream, static_cast<uint4 *>(dst),
+                       static_cast<const uint4 *>(src), nvec);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const size_t done = nvec * 16;
+  if (done < bytes) {
+    return hipMemcpyAsync(static_cast<char *>(dst) + done, static_cast<const char *>(src) + done,
+                          bytes - done, hipMemcpyDeviceToDevice, stream);
+  }
+  return hipSuccess;
 }
 
 hipError_t LaunchFill(void *dst, size_t count, int dtype, double value, hipStream_t stream) {

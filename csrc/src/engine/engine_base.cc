@@ -63,6 +63,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_plane")) device_plane_mode_ = utils::StringToBool(val) ? 1 : 0;
   if (is("rabit_device_sync")) dcfg_.sync = utils::StringToBool(val);
   if (is("rabit_device_timeout_sec")) dcfg_.op_timeout_sec = atof(val);
+  if (is("rabit_device_spin_us")) dcfg_.spin_us = atoi(val);
   if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
@@ -229,9 +230,14 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     dev_->StageToDevice(dst, tmp.data(), bytes);
     return dev_->Finish(MakeProbe());
   }
+  stats_.n_device_ops += 1;
+  if (GetWorldSize() == 1) {
+    // a one-rank reduction is the identity: only materialise it where it was asked for
+    dev_->CopyDeviceAsync(dst, src, bytes);
+    return dev_->Finish(MakeProbe());
+  }
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
-  stats_.n_device_ops += 1;
   s = dev_->Allreduce(src, dst, spec.count, spec.dtype, spec.op, MakeProbe());
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());

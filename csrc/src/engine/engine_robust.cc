@@ -256,8 +256,10 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
     }
     if (CheckAndRecover(s)) {
       if (dev) {
-        dev_->CopyAsync(buf, temp, bytes);
-        dev_->Finish(MakeProbe(), false);  // local copy: order the user stream, no host wait
+        // local copy: order the user stream after it, no host wait.  With one rank the
+        // user buffer already holds the result.
+        if (GetWorldSize() > 1) dev_->CopyDeviceAsync(buf, temp, bytes);
+        dev_->Finish(MakeProbe(), false);
       } else {
         std::memcpy(buf, temp, bytes);
       }
@@ -306,7 +308,7 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
     }
     if (CheckAndRecover(TryBroadcast(buf, total_size, root))) {
       if (dev) {
-        dev_->CopyAsync(temp, buf, total_size);
+        dev_->CopyDeviceAsync(temp, buf, total_size);
         dev_->Finish(MakeProbe(), false);
       } else {
         std::memcpy(temp, buf, total_size);
@@ -360,7 +362,7 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
     // retry after a failure still finds its input
     if (CheckAndRecover(TryAllgather(buf, total_size, slice_begin, slice_end, size_prev_slice))) {
       if (dev) {
-        dev_->CopyAsync(temp, buf, total_size);
+        dev_->CopyDeviceAsync(temp, buf, total_size);
         dev_->Finish(MakeProbe(), false);
       } else {
         std::memcpy(temp, buf, total_size);

@@ -1,0 +1,11 @@
+"""Data-parallel building blocks on top of the rabit engine (rabit is the DP substrate:
+SURVEY §2.9 — every worker holds a shard and Allreduce aggregates statistics).
+
+GradientBuckets   flat HBM gradient buckets (gradients are views into them, so backward
+                  writes straight into the buffers that are reduced: zero packing copies),
+                  one large fault-tolerant allreduce per bucket, averaging fused into the
+                  lazy-prepare kernel.
+FaultTolerantLoop resume-from-checkpoint training loop (LoadCheckPoint / CheckPoint every
+                  k steps), the rabit programming model for iterative jobs.
+"""
+from .data_parallel import FaultTolerantLoop, GradientBuckets  # noqa: F401

@@ -1,0 +1,68 @@
+"""Python API semantics over several CPU ranks, for every library flavour."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from rabit_amd.launcher import LocalJob
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "tests", "scripts", "api_check.py")
+
+
+@pytest.mark.parametrize("lib,extra", [("standard", []), ("base", []), ("mock", []),
+                                      ("standard", ["rabit_elide_consensus=0"]),
+                                      ("standard", ["rabit_reduce_ring_mincount=1"])])
+@pytest.mark.parametrize("n", [1, 3])
+def test_api_world(native_build, lib, extra, n):
+    job = LocalJob([sys.executable, SCRIPT, lib] + extra, n, 1, capture=True, timeout=120,
+                   print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-3000:]
+    assert out.count("API OK") == n
+    assert any("says hi" in m for m in job.tracker.messages)
+
+
+def test_empty_engine_single_process(native_build):
+    import rabit_amd as rabit
+
+    rabit.init(lib="empty")
+    try:
+        assert rabit.get_world_size() == 1 and rabit.engine_name() == "empty"
+        calls = []
+        out = rabit.allreduce(np.ones(3), rabit.SUM, prepare_fun=lambda a: calls.append(1))
+        assert calls == [1] and np.all(out == 1)
+    finally:
+        rabit.finalize()
+
+
+def test_single_node_without_tracker(native_build):
+    import rabit_amd as rabit
+
+    rabit.init()
+    try:
+        assert rabit.get_rank() == 0 and rabit.get_world_size() == 1
+        assert not rabit.is_distributed()
+        assert rabit.broadcast("x", 0) == "x"
+        v, _ = rabit.load_checkpoint()
+        assert v == 0
+        rabit.checkpoint({"a": 1})
+        assert rabit.version_number() == 1
+    finally:
+        rabit.finalize()
+
+
+def test_error_mode_raises(native_build):
+    import rabit_amd as rabit
+
+    rabit.init()
+    rabit.set_error_mode(True)
+    try:
+        with pytest.raises(TypeError):
+            rabit.allreduce(np.ones(2, dtype=np.float16), rabit.SUM)
+        with pytest.raises(TypeError):
+            rabit.allreduce(np.ones(2), rabit.BITOR)
+    finally:
+        rabit.finalize()

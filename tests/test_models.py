@@ -1,0 +1,36 @@
+"""Model families over several CPU ranks, with and without injected failures."""
+import os
+import sys
+
+import pytest
+
+from rabit_amd.launcher import LocalJob
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "tests", "scripts", "models_check.py")
+
+
+def _run(which, n, extra=(), attempts=1):
+    job = LocalJob([sys.executable, SCRIPT, which] + list(extra), n, attempts, capture=True,
+                   timeout=300, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    return rc, job, out
+
+
+@pytest.mark.parametrize("which", ["kmeans", "linear", "gbdt"])
+@pytest.mark.parametrize("n", [1, 3])
+def test_model_trains(native_build, which, n):
+    rc, _, out = _run(which, n)
+    assert rc == 0, out[-3000:]
+    assert out.count("MODEL OK") == n
+
+
+@pytest.mark.parametrize("which,mock", [("kmeans", ["mock=1,3,1,0", "mock=2,5,0,0"]),
+                                        ("gbdt", ["mock=2,2,3,0"]),
+                                        ("linear", ["mock=0,4,2,0"])])
+def test_model_survives_failures(native_build, which, mock):
+    rc, job, out = _run(which, 3, mock, attempts=4)
+    assert rc == 0, out[-3000:]
+    assert out.count("MODEL OK") == 3
+    assert sum(a - 1 for a in job.attempts) >= 1, "kill point not reached"

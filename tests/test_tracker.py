@@ -1,0 +1,104 @@
+"""Tracker topology and launcher behaviour."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from rabit_amd.launcher import LocalJob
+from rabit_amd.tracker import link_map, tree_neighbours
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 7, 8, 10, 16, 31, 64])
+def test_link_map_invariants(n):
+    tree, parent, ring = link_map(n)
+    assert sorted(tree) == list(range(n))
+    # ring is relabelled to rank order
+    for r in range(n):
+        assert ring[r] == ((r - 1) % n, (r + 1) % n)
+    # the tree is symmetric, connected, with one root
+    roots = [r for r in range(n) if parent[r] == -1]
+    assert roots == [0]
+    for r in range(n):
+        for q in tree[r]:
+            assert r in tree[q]
+        if parent[r] != -1:
+            assert parent[r] in tree[r]
+    edges = sum(len(v) for v in tree.values()) // 2
+    assert edges == n - 1
+    seen, stack = {0}, [0]
+    while stack:
+        for q in tree[stack.pop()]:
+            if q not in seen:
+                seen.add(q)
+                stack.append(q)
+    assert len(seen) == n
+
+
+def test_ring_mostly_follows_tree():
+    # the DFS ring should reuse tree edges (short hops) for most ring steps
+    tree, _, ring = link_map(15)
+    shared = sum(1 for r in range(15) if ring[r][1] in tree[r])
+    assert shared >= 8
+
+
+def test_heap_neighbours():
+    assert tree_neighbours(0, 5) == [1, 2]
+    assert tree_neighbours(1, 5) == [0, 3, 4]
+    assert tree_neighbours(4, 5) == [1]
+
+
+def test_launcher_restarts_failing_worker(tmp_path):
+    flag = tmp_path / "died"
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys\n"
+        "t = int(os.environ['DMLC_TASK_ID']); a = int(os.environ['DMLC_NUM_ATTEMPT'])\n"
+        "sys.path.insert(0, %r)\n"
+        "import rabit_amd as rabit\n"
+        "if t == 1 and a == 0:\n"
+        "    open(%r, 'w').write('x'); sys.exit(3)\n"
+        "rabit.init(); rabit.finalize()\n" % (ROOT, str(flag)))
+    job = LocalJob([sys.executable, str(script)], 2, 3, timeout=60, print_fn=lambda m: None)
+    assert job.run() == 0
+    assert flag.exists() and job.attempts == [1, 2]
+
+
+def test_launcher_cli_basic_example(native_build):
+    out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "-n", "3", "--",
+                          os.path.join(native_build, "basic")], capture_output=True, text=True,
+                         timeout=60, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    # Max then Sum of a[i] = rank + i over 3 ranks (doc/guide.md semantics)
+    assert out.stdout.count("after-allreduce-max: a={2, 3, 4}") == 3
+    assert out.stdout.count("after-allreduce-sum: a={6, 9, 12}") == 3
+
+
+def test_examples_broadcast_and_lazy(native_build):
+    out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "-n", "2", "--",
+                          os.path.join(native_build, "broadcast")], capture_output=True,
+                         text=True, timeout=60, cwd=ROOT)
+    assert out.returncode == 0 and out.stdout.count('after-broadcast: s="hello world"') == 2
+    out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "-n", "2", "--",
+                          os.path.join(native_build, "lazy_allreduce")], capture_output=True,
+                         text=True, timeout=60, cwd=ROOT)
+    assert out.returncode == 0
+    assert out.stdout.count("run prepare function") == 2
+    assert out.stdout.count("after-allreduce-sum: a={2, 4, 6}") == 2
+
+
+def test_cpp_unit_tests(native_build):
+    out = subprocess.run([os.path.join(native_build, "unit_tests")], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert " 0 failed" in out.stdout
+
+
+def test_speed_test_cpu(native_build):
+    out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "-n", "4", "--",
+                          os.path.join(native_build, "speed_test"), "100000", "5"],
+                         capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    assert "sum_tdiff-speed" in out.stdout and "bcast_tdiff-speed" in out.stdout
