@@ -43,30 +43,14 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: launch N>1 with "
                          "torch.distributed.run" % (args.gpus, world))
-    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    master_port = int(os.environ.get("MASTER_PORT", "29500"))
-
     import torch
     import rabit_amd as rabit
-    from rabit_amd.tracker import RabitTracker
-
-    tracker = None
-    if rank == 0:
-        # the rabit tracker lives in rank 0; workers find it next to the torchrun master port
-        port = master_port + 17 if world > 1 else 9091
-        tracker = RabitTracker(addr, world, port=port, port_end=port + (1 if world > 1 else 500),
-                               print_fn=lambda m: None)
-        tracker.start(world)
-        tracker_port = tracker.port
-    else:
-        tracker_port = master_port + 17
+    from rabit_amd.torchrun import init_from_env
 
     torch.cuda.set_device(local_rank)
-    rabit.init(lib="standard" if args.engine == "robust" else "base",
-               rabit_tracker_uri=addr, rabit_tracker_port=tracker_port, rabit_task_id=rank,
-               rabit_world_size=world, rabit_device=local_rank, rabit_world1_fastpath=0,
-               DMLC_WORKER_CONNECT_RETRY=20)
-    assert rabit.get_world_size() == world
+    # the rabit tracker lives in rank 0 next to the torchrun master port (rabit_amd.torchrun)
+    ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
+                        rabit_world1_fastpath=0)
     dev = torch.device("cuda", local_rank)
 
     def barrier():
@@ -135,9 +119,7 @@ def main():
     if rank == 0:
         print(json.dumps(rec), flush=True)
     del x
-    rabit.finalize()
-    if tracker is not None:
-        tracker.join(60)
+    ctx.finalize()
 
 
 if __name__ == "__main__":

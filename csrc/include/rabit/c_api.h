@@ -78,6 +78,9 @@ RABIT_DLL void RabitSetErrorMode(int mode);
 RABIT_DLL const char *RabitGetLastError(void);
 /*! \brief engine statistics as a JSON string (recoveries, bytes, per-op timing) */
 RABIT_DLL const char *RabitGetStats(void);
+/*! \brief write the recorded engine spans (rabit_trace=1) as a Chrome trace; returns the span
+ *         count or -1 */
+RABIT_DLL int RabitTraceDump(const char *path);
 
 // ---------------- device kernel entry points (tests / python ops) ----------------
 /*! \brief dst[i] = op(dst[i], src[i]) on device buffers, enqueued on stream */
@@ -92,6 +95,8 @@ RABIT_DLL int RabitDevPrepare(void *dst, void *dst2, const void *src, size_t cou
 /*! \brief 64-bit position-weighted checksum of nbytes (nbytes % 4 == 0) into *out (device u64) */
 RABIT_DLL int RabitDevChecksum(const void *buf, size_t nbytes, void *out_dev_u64,
                                void *hip_stream);
+/*! \brief HBM-to-HBM copy with the gfx950 copy kernel */
+RABIT_DLL int RabitDevCopy(void *dst, const void *src, size_t nbytes, void *hip_stream);
 /*! \brief fill count elements with value */
 RABIT_DLL int RabitDevFill(void *dst, size_t count, int enum_dtype, double value,
                            void *hip_stream);

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "coll/host_coll.h"
+#include "core/trace.h"
 #include "device/kernels.h"
 #include "engine/engine_base.h"
 #include "rabit/internal/io.h"
@@ -231,6 +232,15 @@ RABIT_DLL const char *RabitGetStats() {
   return stats.c_str();
 }
 
+RABIT_DLL int RabitTraceDump(const char *path) {
+  const std::string js = rabit::trace::Tracer::Get().ChromeJson();
+  FILE *fp = fopen(path, "w");
+  if (fp == nullptr) return -1;
+  fwrite(js.data(), 1, js.size(), fp);
+  fclose(fp);
+  return static_cast<int>(rabit::trace::Tracer::Get().size());
+}
+
 RABIT_DLL int RabitDevReduce(void *dst, const void *src, size_t count, int enum_dtype,
                              int enum_op, void *hip_stream) {
   return static_cast<int>(rabit::device::LaunchReduce(dst, src, count, enum_dtype, enum_op,
@@ -255,6 +265,11 @@ RABIT_DLL int RabitDevChecksum(const void *buf, size_t nbytes, void *out_dev_u64
   return static_cast<int>(rabit::device::LaunchChecksum(
       buf, nbytes, static_cast<unsigned long long *>(out_dev_u64),
       static_cast<hipStream_t>(hip_stream)));
+}
+
+RABIT_DLL int RabitDevCopy(void *dst, const void *src, size_t nbytes, void *hip_stream) {
+  return static_cast<int>(
+      rabit::device::LaunchCopy(dst, src, nbytes, static_cast<hipStream_t>(hip_stream)));
 }
 
 RABIT_DLL int RabitDevFill(void *dst, size_t count, int enum_dtype, double value,

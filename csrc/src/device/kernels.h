@@ -33,8 +33,9 @@ hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);
 /*!
- * \brief out[0] += sum_i w_i, out[1] += sum_i (i+1) * w_i over 32-bit words (mod 2^64);
- *        nbytes must be a multiple of 4; out must be zeroed by the caller
+ * \brief position-weighted checksum over 16-byte vectors v = (w0, w1, w2, w3) of 32-bit words:
+ *        out[0] += sum of all words, out[1] += sum_v (v+1) * (w0 + 2 w1 + 3 w2 + 4 w3)
+ *        (mod 2^64); nbytes must be a multiple of 16; out must be zeroed by the caller
  */
 hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *out,
                           hipStream_t stream);

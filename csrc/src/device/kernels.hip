@@ -2,21 +2,26 @@
  * \file kernels.hip
  * \brief gfx950 (MI355X, CDNA4) kernels of the device data plane.
  *
- * All kernels here are HBM-bandwidth bound (element-wise: 2-9 bytes moved per FLOP), so
- * the design goal is to stream at the HBM roof (~6.3 TB/s measured on MI355X):
- *  - 64-lane waves, 256-thread workgroups, grid capped at 2048 workgroups
- *    (256 CUs x 8) and grid-stride beyond that;
- *  - 16 bytes per lane per access (global_load_dwordx4 / global_store_dwordx4);
- *  - kUnroll independent 16-byte loads per lane issued before any use, so every wave keeps
- *    several KB in flight (latency hiding by ILP as well as by occupancy);
- *  - the multi-source reduce is templated on the source count so all loads of one
- *    element-vector are issued back to back.
- * MFMA is deliberately not used: an element-wise reduce has no reuse, a ones-vector GEMM
- * over stacked peer buffers moves the same bytes and adds matrix-pipe work.
+ * All kernels here are HBM-bandwidth bound (element-wise: no reuse), so the goal is the HBM
+ * roof (~6.3-7 TB/s achievable on MI355X).  Structure, chosen by measurement
+ * (tools/kernel_variants.hip, profiles/r1_s3_variants): a one-shot grid in which workgroup b
+ * owns the contiguous tile of 256 x U 16-byte vectors starting at b*256*U:
+ *  - every wave instruction moves 1 KiB contiguous (64 lanes x 16 B: global_load_dwordx4);
+ *  - all U (x sources) loads of a lane are issued before any arithmetic or store;
+ *  - the data is loaded as uint4 and re-interpreted in registers, so the compiler cannot split
+ *    a 16-byte access into halves (it did with struct-of-T packs: 4.8 TB/s, half-width stores);
+ *  - no grid-stride loop: 8192 workgroups for 128 MiB; the dispatcher balances them over the
+ *    256 CUs / 8 XCDs (grid-stride at 2048 workgroups measured 5.0 TB/s for dst += src vs 6.9);
+ *  - default cache policy: nontemporal loads/stores measured 6-9 % slower.
+ * MFMA is deliberately not used: an element-wise reduce has no data reuse; a ones-vector GEMM
+ * over stacked peer buffers moves the same bytes and only adds matrix-pipe work.
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "device/kernels.h"
@@ -26,8 +31,6 @@ namespace device {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kMaxGrid = 2048;
-constexpr int kUnroll = 4;
 
 enum OpCode : int { kOpMax = 0, kOpMin = 1, kOpSum = 2, kOpOr = 3 };
 
@@ -50,67 +53,69 @@ struct Apply<T, kOpOr> {
   __device__ __forceinline__ static T f(T a, T b) { return a | b; }
 };
 
-/*! \brief 16-byte pack of T */
-template <typename T>
-struct alignas(16) Pack {
-  static constexpr int kLanes = 16 / sizeof(T);
-  T v[kLanes];
-};
-
-inline int GridFor(size_t items) {
-  size_t blocks = (items + kBlock - 1) / kBlock;
-  if (blocks < 1) blocks = 1;
-  if (blocks > static_cast<size_t>(kMaxGrid)) blocks = kMaxGrid;
-  return static_cast<int>(blocks);
+/*! \brief lane-wise op on the T lanes of two 16-byte vectors */
+template <typename T, int OP>
+__device__ __forceinline__ uint4 Combine(uint4 a, uint4 b) {
+  constexpr int L = 16 / sizeof(T);
+  T x[L], y[L];
+  __builtin_memcpy(x, &a, 16);
+  __builtin_memcpy(y, &b, 16);
+#pragma unroll
+  for (int j = 0; j < L; ++j) x[j] = Apply<T, OP>::f(x[j], y[j]);
+  uint4 r;
+  __builtin_memcpy(&r, x, 16);
+  return r;
 }
 
 inline bool Aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+/*! \brief workgroups for a one-shot tile grid over nvec vectors (>= 1) */
+inline unsigned TileGrid(size_t nvec, int unroll) {
+  size_t per = static_cast<size_t>(kBlock) * unroll;
+  size_t g = (nvec + per - 1) / per;
+  return static_cast<unsigned>(g == 0 ? 1 : g);
+}
+
+/*! \brief elements past the last full 16-byte vector, handled by workgroup 0 */
+template <typename T, typename F>
+__device__ __forceinline__ void Tail(size_t nvec, size_t n, F &&f) {
+  constexpr size_t L = 16 / sizeof(T);
+  if (blockIdx.x == 0) {
+    for (size_t i = nvec * L + threadIdx.x; i < n; i += kBlock) f(i);
+  }
+}
+
 // ---------------------------------------------------------------- two-operand reduce
-template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void ReduceVecKernel(T *__restrict__ dst,
-                                                          const T *__restrict__ src, size_t n) {
-  using P = Pack<T>;
-  constexpr int L = P::kLanes;
-  const size_t nvec = n / L;
-  P *d = reinterpret_cast<P *>(dst);
-  const P *s = reinterpret_cast<const P *>(src);
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
-    P a[kUnroll], b[kUnroll];
+template <typename T, int OP, int U>
+__global__ __launch_bounds__(kBlock) void ReduceTileKernel(T *__restrict__ dst,
+                                                           const T *__restrict__ src, size_t n) {
+  const size_t nvec = n * sizeof(T) / 16;
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
+  if (base + (U - 1) * kBlock < nvec) {
+    uint4 a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      a[u] = d[i + u * stride];
-      b[u] = s[i + u * stride];
-    }
+    for (int u = 0; u < U; ++u) a[u] = d[base + u * kBlock];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) b[u] = s[base + u * kBlock];
 #pragma unroll
-      for (int j = 0; j < L; ++j) a[u].v[j] = Apply<T, OP>::f(a[u].v[j], b[u].v[j]);
-      d[i + u * stride] = a[u];
+    for (int u = 0; u < U; ++u) d[base + u * kBlock] = Combine<T, OP>(a[u], b[u]);
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * kBlock;
+      if (i < nvec) d[i] = Combine<T, OP>(d[i], s[i]);
     }
   }
-  for (; i < nvec; i += stride) {
-    P a = d[i], b = s[i];
-#pragma unroll
-    for (int j = 0; j < L; ++j) a.v[j] = Apply<T, OP>::f(a.v[j], b.v[j]);
-    d[i] = a;
-  }
-  // tail (< L elements), first threads of the grid
-  const size_t tail = nvec * L;
-  const size_t t = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (tail + t < n) dst[tail + t] = Apply<T, OP>::f(dst[tail + t], src[tail + t]);
+  Tail<T>(nvec, n, [&](size_t i) { dst[i] = Apply<T, OP>::f(dst[i], src[i]); });
 }
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void ReduceScalarKernel(T *__restrict__ dst,
                                                              const T *__restrict__ src,
                                                              size_t n) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    dst[i] = Apply<T, OP>::f(dst[i], src[i]);
-  }
+  const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) dst[i] = Apply<T, OP>::f(dst[i], src[i]);
 }
 
 template <typename T, int OP>
@@ -118,12 +123,12 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
   T *d = static_cast<T *>(dst);
   const T *s = static_cast<const T *>(src);
   if (Aligned16(dst) && Aligned16(src)) {
-    const size_t nvec = n / Pack<T>::kLanes;
-    hipLaunchKernelGGL((ReduceVecKernel<T, OP>), dim3(GridFor((nvec + kUnroll - 1) / kUnroll)),
+    constexpr int U = 4;
+    hipLaunchKernelGGL((ReduceTileKernel<T, OP, U>), dim3(TileGrid(n * sizeof(T) / 16, U)),
                        dim3(kBlock), 0, st, d, s, n);
   } else {
-    hipLaunchKernelGGL((ReduceScalarKernel<T, OP>), dim3(GridFor(n)), dim3(kBlock), 0, st, d, s,
-                       n);
+    hipLaunchKernelGGL((ReduceScalarKernel<T, OP>), dim3(TileGrid(n, 1)), dim3(kBlock), 0, st, d,
+                       s, n);
   }
   return hipGetLastError();
 }
@@ -133,55 +138,60 @@ struct SrcList {
   const void *p[kMaxReduceSources];
 };
 
-template <typename T, int OP, int NSRC>
-__global__ __launch_bounds__(kBlock) void ReduceMultiVecKernel(T *dst, SrcList srcs,
-                                                               size_t n) {
-  using P = Pack<T>;
-  constexpr int L = P::kLanes;
-  const size_t nvec = n / L;
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec;
-       i += stride) {
-    P x[NSRC];
+template <typename T, int OP, int NSRC, int U>
+__global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList srcs, size_t n) {
+  const size_t nvec = n * sizeof(T) / 16;
+  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  if (base + (U - 1) * kBlock < nvec) {
+    uint4 x[NSRC][U];
 #pragma unroll
-    for (int k = 0; k < NSRC; ++k) x[k] = reinterpret_cast<const P *>(srcs.p[k])[i];
-    P acc = x[0];
+    for (int k = 0; k < NSRC; ++k) {
 #pragma unroll
-    for (int k = 1; k < NSRC; ++k) {
-#pragma unroll
-      for (int j = 0; j < L; ++j) acc.v[j] = Apply<T, OP>::f(acc.v[j], x[k].v[j]);
+      for (int u = 0; u < U; ++u) x[k][u] = reinterpret_cast<const uint4 *>(srcs.p[k])[base + u * kBlock];
     }
-    reinterpret_cast<P *>(dst)[i] = acc;
-  }
-  const size_t tail = nvec * L;
-  const size_t t = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (tail + t < n) {
-    T acc = static_cast<const T *>(srcs.p[0])[tail + t];
 #pragma unroll
-    for (int k = 1; k < NSRC; ++k) {
-      acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[tail + t]);
+    for (int u = 0; u < U; ++u) {
+      uint4 acc = x[0][u];
+#pragma unroll
+      for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, x[k][u]);
+      d[base + u * kBlock] = acc;
     }
-    dst[tail + t] = acc;
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * kBlock;
+      if (i >= nvec) break;
+      uint4 acc = reinterpret_cast<const uint4 *>(srcs.p[0])[i];
+      for (int k = 1; k < NSRC; ++k) {
+        acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(srcs.p[k])[i]);
+      }
+      d[i] = acc;
+    }
   }
+  Tail<T>(nvec, n, [&](size_t i) {
+    T acc = static_cast<const T *>(srcs.p[0])[i];
+#pragma unroll
+    for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
+    dst[i] = acc;
+  });
 }
 
 template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst,
-                                                                  SrcList srcs, int nsrc,
+__global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcList srcs, int nsrc,
                                                                   size_t n) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    T acc = static_cast<const T *>(srcs.p[0])[i];
-    for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
-    dst[i] = acc;
-  }
+  const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  T acc = static_cast<const T *>(srcs.p[0])[i];
+  for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
+  dst[i] = acc;
 }
 
 template <typename T, int OP, int NSRC>
-void LaunchMultiVec(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
-  const size_t nvec = n / Pack<T>::kLanes;
-  hipLaunchKernelGGL((ReduceMultiVecKernel<T, OP, NSRC>), dim3(GridFor(nvec)), dim3(kBlock), 0,
-                     st, dst, sl, n);
+void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
+  // keep ~8 16-byte loads in flight per lane
+  constexpr int U = NSRC >= 8 ? 1 : (NSRC >= 4 ? 2 : 4);
+  hipLaunchKernelGGL((ReduceMultiTileKernel<T, OP, NSRC, U>),
+                     dim3(TileGrid(n * sizeof(T) / 16, U)), dim3(kBlock), 0, st, dst, sl, n);
 }
 
 template <typename T, int OP>
@@ -194,19 +204,19 @@ hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, h
   }
   T *d = static_cast<T *>(dst);
   if (!aligned) {
-    hipLaunchKernelGGL((ReduceMultiScalarKernel<T, OP>), dim3(GridFor(n)), dim3(kBlock), 0, st, d,
-                       sl, nsrc, n);
+    hipLaunchKernelGGL((ReduceMultiScalarKernel<T, OP>), dim3(TileGrid(n, 1)), dim3(kBlock), 0, st,
+                       d, sl, nsrc, n);
     return hipGetLastError();
   }
   switch (nsrc) {
-    case 1: LaunchMultiVec<T, OP, 1>(d, sl, n, st); break;
-    case 2: LaunchMultiVec<T, OP, 2>(d, sl, n, st); break;
-    case 3: LaunchMultiVec<T, OP, 3>(d, sl, n, st); break;
-    case 4: LaunchMultiVec<T, OP, 4>(d, sl, n, st); break;
-    case 5: LaunchMultiVec<T, OP, 5>(d, sl, n, st); break;
-    case 6: LaunchMultiVec<T, OP, 6>(d, sl, n, st); break;
-    case 7: LaunchMultiVec<T, OP, 7>(d, sl, n, st); break;
-    case 8: LaunchMultiVec<T, OP, 8>(d, sl, n, st); break;
+    case 1: LaunchMultiTile<T, OP, 1>(d, sl, n, st); break;
+    case 2: LaunchMultiTile<T, OP, 2>(d, sl, n, st); break;
+    case 3: LaunchMultiTile<T, OP, 3>(d, sl, n, st); break;
+    case 4: LaunchMultiTile<T, OP, 4>(d, sl, n, st); break;
+    case 5: LaunchMultiTile<T, OP, 5>(d, sl, n, st); break;
+    case 6: LaunchMultiTile<T, OP, 6>(d, sl, n, st); break;
+    case 7: LaunchMultiTile<T, OP, 7>(d, sl, n, st); break;
+    case 8: LaunchMultiTile<T, OP, 8>(d, sl, n, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -218,58 +228,69 @@ __device__ __forceinline__ T PrepApply(T x, int prep, T alpha) {
   switch (prep) {
     case kPrepSquare: return x * x;
     case kPrepScale: return x * alpha;
-    case kPrepAbs: return x < T(0) ? T(0) - x : x;
+    case kPrepAbs:
+      if constexpr (std::is_signed<T>::value) return x < T(0) ? T(0) - x : x;
+      return x;
     default: return x;
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void PrepareVecKernel(T *__restrict__ dst,
-                                                           T *__restrict__ dst2,
-                                                           const T *__restrict__ src, size_t n,
-                                                           int prep, T alpha) {
-  using P = Pack<T>;
-  constexpr int L = P::kLanes;
-  const size_t nvec = n / L;
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
-    P a[kUnroll];
+__device__ __forceinline__ uint4 PrepVec(uint4 v, int prep, T alpha) {
+  constexpr int L = 16 / sizeof(T);
+  T x[L];
+  __builtin_memcpy(x, &v, 16);
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = reinterpret_cast<const P *>(src)[i + u * stride];
+  for (int j = 0; j < L; ++j) x[j] = PrepApply<T>(x[j], prep, alpha);
+  uint4 r;
+  __builtin_memcpy(&r, x, 16);
+  return r;
+}
+
+template <typename T, int U>
+__global__ __launch_bounds__(kBlock) void PrepareTileKernel(T *dst, T *dst2, const T *src,
+                                                            size_t n, int prep, T alpha) {
+  const size_t nvec = n * sizeof(T) / 16;
+  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  uint4 *d2 = reinterpret_cast<uint4 *>(dst2);
+  if (base + (U - 1) * kBlock < nvec) {
+    uint4 a[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) a[u] = s[base + u * kBlock];
 #pragma unroll
-      for (int j = 0; j < L; ++j) a[u].v[j] = PrepApply<T>(a[u].v[j], prep, alpha);
-      reinterpret_cast<P *>(dst)[i + u * stride] = a[u];
-      if (dst2 != nullptr) reinterpret_cast<P *>(dst2)[i + u * stride] = a[u];
+    for (int u = 0; u < U; ++u) a[u] = PrepVec<T>(a[u], prep, alpha);
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[base + u * kBlock] = a[u];
+    if (d2 != nullptr) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) d2[base + u * kBlock] = a[u];
+    }
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * kBlock;
+      if (i >= nvec) break;
+      const uint4 y = PrepVec<T>(s[i], prep, alpha);
+      d[i] = y;
+      if (d2 != nullptr) d2[i] = y;
     }
   }
-  for (; i < nvec; i += stride) {
-    P a = reinterpret_cast<const P *>(src)[i];
-#pragma unroll
-    for (int j = 0; j < L; ++j) a.v[j] = PrepApply<T>(a.v[j], prep, alpha);
-    reinterpret_cast<P *>(dst)[i] = a;
-    if (dst2 != nullptr) reinterpret_cast<P *>(dst2)[i] = a;
-  }
-  const size_t tail = nvec * L;
-  const size_t t = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (tail + t < n) {
-    T y = PrepApply<T>(src[tail + t], prep, alpha);
-    dst[tail + t] = y;
-    if (dst2 != nullptr) dst2[tail + t] = y;
-  }
+  Tail<T>(nvec, n, [&](size_t i) {
+    const T y = PrepApply<T>(src[i], prep, alpha);
+    dst[i] = y;
+    if (dst2 != nullptr) dst2[i] = y;
+  });
 }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void PrepareScalarKernel(T *dst, T *dst2, const T *src,
                                                               size_t n, int prep, T alpha) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    T y = PrepApply<T>(src[i], prep, alpha);
-    dst[i] = y;
-    if (dst2 != nullptr) dst2[i] = y;
-  }
+  const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const T y = PrepApply<T>(src[i], prep, alpha);
+  dst[i] = y;
+  if (dst2 != nullptr) dst2[i] = y;
 }
 
 template <typename T>
@@ -280,36 +301,46 @@ hipError_t Prepare(void *dst, void *dst2, const void *src, size_t n, int prep, d
   const T *s = static_cast<const T *>(src);
   const T a = static_cast<T>(alpha);
   if (Aligned16(dst) && Aligned16(src) && (dst2 == nullptr || Aligned16(dst2))) {
-    const size_t nvec = n / Pack<T>::kLanes;
-    hipLaunchKernelGGL(PrepareVecKernel<T>, dim3(GridFor((nvec + kUnroll - 1) / kUnroll)),
+    constexpr int U = 4;
+    hipLaunchKernelGGL((PrepareTileKernel<T, U>), dim3(TileGrid(n * sizeof(T) / 16, U)),
                        dim3(kBlock), 0, st, d, d2, s, n, prep, a);
   } else {
-    hipLaunchKernelGGL(PrepareScalarKernel<T>, dim3(GridFor(n)), dim3(kBlock), 0, st, d, d2, s, n,
-                       prep, a);
+    hipLaunchKernelGGL(PrepareScalarKernel<T>, dim3(TileGrid(n, 1)), dim3(kBlock), 0, st, d, d2, s,
+                       n, prep, a);
   }
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- copy
+template <int U>
+__global__ __launch_bounds__(kBlock) void CopyTileKernel(uint4 *__restrict__ dst,
+                                                        const uint4 *__restrict__ src,
+                                                        size_t nvec) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
+  if (base + (U - 1) * kBlock < nvec) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[base + u * kBlock];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[base + u * kBlock] = v[u];
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * kBlock;
+      if (i < nvec) dst[i] = src[i];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- checksum
-__global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint32_t *__restrict__ w,
-                                                         size_t nwords,
-                                                         unsigned long long *__restrict__ out) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  unsigned long long s1 = 0, s2 = 0;
-  const size_t nvec = nwords / 4;
-  const uint4 *w4 = reinterpret_cast<const uint4 *>(w);
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
-    uint4 v = w4[i];
-    const unsigned long long base = 4ull * i + 1ull;
-    s1 += static_cast<unsigned long long>(v.x) + v.y + v.z + v.w;
-    s2 += base * v.x + (base + 1) * v.y + (base + 2) * v.z + (base + 3) * v.w;
-  }
-  const size_t t = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (4 * nvec + t < nwords) {
-    s1 += w[4 * nvec + t];
-    s2 += (4ull * nvec + t + 1ull) * w[4 * nvec + t];
-  }
-  // wave64 reduction, then across the 4 waves of the workgroup through LDS
+/*!
+ * Position-weighted checksum over 16-byte vectors v (words w0..w3):
+ *   s1 = sum of all 32-bit words,  s2 = sum_v (v+1) * (w0 + 2 w1 + 3 w2 + 4 w3)   (mod 2^64)
+ * One 64-bit multiply per 16 bytes keeps it bandwidth-bound; order changes across vectors
+ * and within a vector both change s2.
+ */
+constexpr int kChecksumGrid = 1024;  // 4 workgroups per CU, tiles walked grid-stride
+
+__device__ __forceinline__ void BlockSum2(unsigned long long &s1, unsigned long long &s2) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s1 += __shfl_down(s1, off, 64);
@@ -323,41 +354,68 @@ __global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint32_t *__restr
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long a = 0, b = 0;
+    s1 = s2 = 0;
 #pragma unroll
     for (int k = 0; k < kBlock / 64; ++k) {
-      a += part[0][k];
-      b += part[1][k];
+      s1 += part[0][k];
+      s2 += part[1][k];
     }
-    atomicAdd(&out[0], a);
-    atomicAdd(&out[1], b);
   }
 }
 
-// ---------------------------------------------------------------- copy
-/*! \brief 16-byte-per-lane streaming copy, kUnroll loads in flight per lane */
-__global__ __launch_bounds__(kBlock) void CopyVecKernel(uint4 *__restrict__ dst,
-                                                       const uint4 *__restrict__ src,
-                                                       size_t nvec) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
-    uint4 v[kUnroll];
+/*! \brief pass 1: each workgroup folds its tiles into one (s1, s2) partial (no atomics: 8192
+ *  workgroups adding into one word serialise, measured 3.3x slower than this two-pass form) */
+template <int U>
+__global__ __launch_bounds__(kBlock) void ChecksumPartialKernel(const uint4 *__restrict__ w,
+                                                               size_t nvec,
+                                                               unsigned long long *partial) {
+  unsigned long long s1 = 0, s2 = 0;
+  const size_t ntile = (nvec + static_cast<size_t>(kBlock) * U - 1) / (kBlock * U);
+  for (size_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const size_t base = t * kBlock * U + threadIdx.x;
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * kBlock;
+      v[u] = i < nvec ? w[i] : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) dst[i + u * stride] = v[u];
+    for (int u = 0; u < U; ++u) {
+      const unsigned long long idx = base + u * kBlock + 1ull;
+      const unsigned long long q = static_cast<unsigned long long>(v[u].x) + 2ull * v[u].y +
+                                   3ull * v[u].z + 4ull * v[u].w;
+      s1 += static_cast<unsigned long long>(v[u].x) + v[u].y + v[u].z + v[u].w;
+      s2 += idx * q;
+    }
   }
-  for (; i < nvec; i += stride) dst[i] = src[i];
+  BlockSum2(s1, s2);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = s1;
+    partial[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+/*! \brief pass 2: one workgroup adds the partials into out */
+__global__ __launch_bounds__(kBlock) void ChecksumFinishKernel(const unsigned long long *partial,
+                                                              int nparts,
+                                                              unsigned long long *out) {
+  unsigned long long s1 = 0, s2 = 0;
+  for (int i = threadIdx.x; i < nparts; i += kBlock) {
+    s1 += partial[2 * i];
+    s2 += partial[2 * i + 1];
+  }
+  BlockSum2(s1, s2);
+  if (threadIdx.x == 0) {
+    out[0] += s1;
+    out[1] += s2;
+  }
 }
 
 // ---------------------------------------------------------------- fill
 template <typename T>
 __global__ __launch_bounds__(kBlock) void FillKernel(T *dst, size_t n, T value) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    dst[i] = value;
-  }
+  const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) dst[i] = value;
 }
 
 // dtype code -> C++ type; integer-only ops reject float types
@@ -381,24 +439,12 @@ hipError_t DispatchType(int dtype, bool int_only, Fn &&fn) {
 template <typename T>
 struct OrTag {
   // BitOR is only instantiated for integral types
-  template <typename U = T>
-  static typename std::enable_if<std::is_integral<U>::value, hipError_t>::type Reduce2Or(
-      void *d, const void *s, size_t n, hipStream_t st) {
-    return Reduce2<U, kOpOr>(d, s, n, st);
-  }
-  template <typename U = T>
-  static typename std::enable_if<!std::is_integral<U>::value, hipError_t>::type Reduce2Or(
-      void *, const void *, size_t, hipStream_t) {
+  static hipError_t Reduce2Or(void *d, const void *s, size_t n, hipStream_t st) {
+    if constexpr (std::is_integral<T>::value) return Reduce2<T, kOpOr>(d, s, n, st);
     return hipErrorInvalidValue;
   }
-  template <typename U = T>
-  static typename std::enable_if<std::is_integral<U>::value, hipError_t>::type MultiOr(
-      void *d, const void *const *s, int k, size_t n, hipStream_t st) {
-    return ReduceMulti<U, kOpOr>(d, s, k, n, st);
-  }
-  template <typename U = T>
-  static typename std::enable_if<!std::is_integral<U>::value, hipError_t>::type MultiOr(
-      void *, const void *const *, int, size_t, hipStream_t) {
+  static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st) {
+    if constexpr (std::is_integral<T>::value) return ReduceMulti<T, kOpOr>(d, s, k, n, st);
     return hipErrorInvalidValue;
   }
 };
@@ -444,23 +490,13 @@ hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, i
   });
 }
 
-hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *out,
-                          hipStream_t stream) {
-  if (nbytes % 4 != 0 || !Aligned16(buf)) return hipErrorInvalidValue;
-  const size_t nwords = nbytes / 4;
-  if (nwords == 0) return hipSuccess;
-  hipLaunchKernelGGL(ChecksumKernel, dim3(GridFor(nwords / 4 + 1)), dim3(kBlock), 0, stream,
-                     static_cast<const uint32_t *>(buf), nwords, out);
-  return hipGetLastError();
-}
-
 hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stream) {
   if (bytes == 0 || dst == src) return hipSuccess;
   const size_t nvec = Aligned16(dst) && Aligned16(src) ? bytes / 16 : 0;
   if (nvec != 0) {
-    hipLaunchKernelGGL(CopyVecKernel, dim3(GridFor((nvec + kUnroll - 1) / kUnroll)),
-                       dim3(kBlock), 0, stream, static_cast<uint4 *>(dst),
-                       static_cast<const uint4 *>(src), nvec);
+    constexpr int U = 4;
+    hipLaunchKernelGGL(CopyTileKernel<U>, dim3(TileGrid(nvec, U)), dim3(kBlock), 0, stream,
+                       static_cast<uint4 *>(dst), static_cast<const uint4 *>(src), nvec);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -472,11 +508,43 @@ hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stre
   return hipSuccess;
 }
 
+hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *out,
+                          hipStream_t stream) {
+  if (nbytes % 16 != 0 || !Aligned16(buf)) return hipErrorInvalidValue;
+  const size_t nvec = nbytes / 16;
+  if (nvec == 0) return hipSuccess;
+  // per-device partials scratch (2 x kChecksumGrid u64), allocated once per device
+  static std::mutex mu;
+  static std::map<int, unsigned long long *> scratch;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  unsigned long long *partial;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = scratch.find(dev);
+    if (it == scratch.end()) {
+      void *p = nullptr;
+      e = hipMalloc(&p, sizeof(unsigned long long) * 2 * kChecksumGrid);
+      if (e != hipSuccess) return e;
+      it = scratch.emplace(dev, static_cast<unsigned long long *>(p)).first;
+    }
+    partial = it->second;
+  }
+  constexpr int U = 4;
+  const unsigned grid = std::min<unsigned>(TileGrid(nvec, U), kChecksumGrid);
+  hipLaunchKernelGGL(ChecksumPartialKernel<U>, dim3(grid), dim3(kBlock), 0, stream,
+                     static_cast<const uint4 *>(buf), nvec, partial);
+  hipLaunchKernelGGL(ChecksumFinishKernel, dim3(1), dim3(kBlock), 0, stream,
+                     static_cast<const unsigned long long *>(partial), static_cast<int>(grid), out);
+  return hipGetLastError();
+}
+
 hipError_t LaunchFill(void *dst, size_t count, int dtype, double value, hipStream_t stream) {
   if (count == 0) return hipSuccess;
   return DispatchType(dtype, false, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;
-    hipLaunchKernelGGL(FillKernel<T>, dim3(GridFor(count)), dim3(kBlock), 0, stream,
+    hipLaunchKernelGGL(FillKernel<T>, dim3(TileGrid(count, 1)), dim3(kBlock), 0, stream,
                        static_cast<T *>(dst), count, static_cast<T>(value));
     return hipGetLastError();
   });

@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "core/params.h"
+#include "core/trace.h"
 #include "device/kernels.h"
 #include "rabit/internal/timer.h"
 #include "rabit/internal/utils.h"
@@ -68,6 +69,9 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
+  if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
+  if (is("rabit_trace_roctx")) trace_roctx_ = utils::StringToBool(val);
+  if (is("rabit_trace_capacity")) trace_capacity_ = static_cast<size_t>(atol(val));
 }
 
 bool EngineBase::Init(int argc, char *argv[]) {
@@ -108,6 +112,7 @@ bool EngineBase::Init(int argc, char *argv[]) {
     exit(0);
   }
   utils::Check(topo_.links.empty(), "can only call Init once");
+  trace::Tracer::Get().Configure(trace_spans_, trace_roctx_, trace_capacity_);
   rank_ = -1;
   host_uri_ = net::HostName();
   if (!ReconnectLinks("start")) return false;
@@ -231,6 +236,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     return dev_->Finish(MakeProbe());
   }
   stats_.n_device_ops += 1;
+  trace::Scope ts("device_allreduce", rank_, version_number_, seq_counter_, bytes, 1);
   if (GetWorldSize() == 1) {
     // a one-rank reduction is the identity: only materialise it where it was asked for
     dev_->CopyDeviceAsync(dst, src, bytes);

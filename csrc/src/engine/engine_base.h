@@ -134,6 +134,9 @@ class EngineBase : public IEngine {
   bool timeout_enabled_{false};
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
+  bool trace_spans_{false};
+  bool trace_roctx_{false};
+  size_t trace_capacity_{1 << 16};
   // runtime state
   net::Topology topo_;
   std::unique_ptr<coll::HostCollectives> host_;

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstring>
 
+#include "core/trace.h"
 #include "device/kernels.h"
 #include "rabit/internal/io.h"
 #include "rabit/internal/timer.h"
@@ -236,6 +237,7 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
     return;
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("allreduce", rank_, version_number_, seq_counter_, bytes, dev);
   bool recovered = RecoverExec(buf, bytes, 0, seq_counter_, cur_cache_seq_, "Allreduce");
   ApplyRetention();
   if (!recovered) run_prepare();
@@ -297,6 +299,7 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
     return;
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("broadcast", rank_, version_number_, seq_counter_, total_size, dev);
   bool recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Broadcast");
   ApplyRetention();
   void *temp = resbuf_.AllocTemp(total_size, dev);
@@ -349,6 +352,7 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
     return;
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("allgather", rank_, version_number_, seq_counter_, total_size, dev);
   bool recovered = RecoverExec(buf, total_size, 0, seq_counter_, cur_cache_seq_, "Allgather");
   ApplyRetention();
   void *temp = resbuf_.AllocTemp(total_size, dev);
@@ -415,6 +419,7 @@ int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local
                  "need to set rabit_local_replica larger than 1 to checkpoint local_model");
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("load_checkpoint", rank_, version_number_, seq_counter_, 0, 0);
   if (RecoverExec(nullptr, 0, ActionSummary::kLoadCheck, ActionSummary::kSpecialOp,
                   cur_cache_seq_, "LoadCheckPoint")) {
     const int nlocal =
@@ -470,6 +475,7 @@ void EngineRobust::CheckPointImpl(const Serializable *global_model,
     return;
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("checkpoint", rank_, version_number_, seq_counter_, 0, 0);
   LocalModelCheck(local_model != nullptr);
   if (num_local_replica_ == 0) {
     utils::Check(local_model == nullptr,

@@ -20,6 +20,7 @@
 #include <thread>
 #include <utility>
 
+#include "core/trace.h"
 #include "engine/engine_robust.h"
 #include "rabit/internal/io.h"
 #include "rabit/internal/timer.h"
@@ -35,6 +36,7 @@ bool EngineRobust::CheckAndRecover(Status s) {
     return true;
   }
   const double t0 = utils::GetTime();
+  trace::Scope ts("recover", rank_, version_number_, seq_counter_, 0, 0);
   fast_mode_ = false;
   recover_counter_ += 1;
   stats_.n_recover_events += 1;
@@ -291,6 +293,7 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
                   "TryGetResult: local checkpoint state");
     return TryRecoverLocalState(&local_rptr_[nv], &local_chkpt_[nv]);
   }
+  trace::Scope ts("replay", rank_, version_number_, seqno, size, 0);
   RecoverType role;
   void *data = nullptr;
   bool data_dev = false;
@@ -552,7 +555,11 @@ bool EngineRobust::RecoverExec(void *buf, size_t size, int flag, int seqno, int 
     ReportStatus();
     ActionSummary act = req;
     const double t0 = utils::GetTime();
-    Status s = host_->TreeAllreduce(&act, sizeof(act), 1, ActionSummary::Reducer);
+    Status s;
+    {
+      trace::Scope ts("consensus", rank_, version_number_, seqno, sizeof(act), 0);
+      s = host_->TreeAllreduce(&act, sizeof(act), 1, ActionSummary::Reducer);
+    }
     stats_.n_consensus += 1;
     stats_.t_consensus += utils::GetTime() - t0;
     if (!CheckAndRecover(s)) continue;

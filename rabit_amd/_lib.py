@@ -72,6 +72,7 @@ def _declare(d: ctypes.CDLL) -> None:
         "RabitSetErrorMode": (None, [c_int]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),
+        "RabitTraceDump": (c_int, [c_char_p]),
         "RabitDevReduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
         "RabitDevReduceMulti": (c_int, [c_void_p, ctypes.POINTER(c_void_p), c_int, c_size_t,
                                         c_int, c_int, c_void_p]),
@@ -79,6 +80,7 @@ def _declare(d: ctypes.CDLL) -> None:
                                     c_double, c_void_p]),
         "RabitDevChecksum": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
         "RabitDevFill": (c_int, [c_void_p, c_size_t, c_int, c_double, c_void_p]),
+        "RabitDevCopy": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(d, name)

@@ -334,6 +334,13 @@ def stats() -> dict:
     return json.loads(_LIB.RabitGetStats().decode())
 
 
+def dump_trace(path: str) -> int:
+    """Write the engine's span log (init with rabit_trace=1) as a Chrome trace JSON file;
+    returns the number of spans."""
+    _check_init()
+    return _LIB.RabitTraceDump(path.encode())
+
+
 def last_error() -> str:
     if _LIB is None:
         return ""

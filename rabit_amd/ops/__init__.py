@@ -86,6 +86,15 @@ def checksum(buf):
     return out
 
 
+def copy(dst, src):
+    """dst <- src (bytes of src), gfx950 copy kernel."""
+    nbytes = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() >= nbytes
+    _check(_dll().RabitDevCopy(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                               nbytes, _stream(dst)), "RabitDevCopy")
+    return dst
+
+
 def fill(dst, value: float):
     _check(_dll().RabitDevFill(ctypes.c_void_p(dst.data_ptr()), dst.numel(), dtype_enum(dst),
                                float(value), _stream(dst)), "RabitDevFill")

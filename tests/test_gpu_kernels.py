@@ -92,13 +92,33 @@ def test_prepare(dev, prep, fn):
     torch.testing.assert_close(dst2, fn(src))
 
 
-def test_checksum(dev):
-    x = _rand(12345, torch.int32, dev, 9)
+@pytest.mark.parametrize("n", [4, 12344, 1 << 20])
+def test_checksum(dev, n):
+    x = _rand(n, torch.int32, dev, 9)
     got = ops.checksum(x).cpu().numpy().view(np.uint64)
-    w = x.cpu().numpy().view(np.uint32).astype(np.uint64)
+    w = x.cpu().numpy().view(np.uint32).astype(np.uint64).reshape(-1, 4)
     s1 = np.sum(w, dtype=np.uint64)
-    s2 = np.sum(w * np.arange(1, w.size + 1, dtype=np.uint64), dtype=np.uint64)
+    q = w[:, 0] + 2 * w[:, 1] + 3 * w[:, 2] + 4 * w[:, 3]
+    s2 = np.sum(q * np.arange(1, w.shape[0] + 1, dtype=np.uint64), dtype=np.uint64)
     assert got[0] == s1 and got[1] == s2
+
+
+def test_checksum_detects_swap(dev):
+    x = _rand(4096, torch.int32, dev, 11)
+    y = x.clone()
+    y[[0, 4]] = y[[4, 0]]
+    if torch.equal(x, y):
+        pytest.skip("degenerate data")
+    assert not torch.equal(ops.checksum(x), ops.checksum(y))
+
+
+@pytest.mark.parametrize("nbytes", [16, 1000, (1 << 20) + 8])
+def test_copy_kernel(dev, nbytes):
+    src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=dev)
+    dst = torch.zeros_like(src)
+    ops.copy(dst, src)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
 
 
 def test_fill(dev):

@@ -1,0 +1,30 @@
+"""The torchrun launch path used by bench.py (tracker hosted by rank 0), on CPU ranks."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_torchrun_rendezvous(native_build, n):
+    port = _free_port()
+    env = dict(os.environ, rabit_device_plane="0")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+                          "--master-port", str(port),
+                          os.path.join(ROOT, "tests", "scripts", "torchrun_check.py")],
+                         capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.count("TORCHRUN OK") == n

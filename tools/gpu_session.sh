@@ -26,6 +26,13 @@ for s in $STEPS; do
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python3 bench.py --steps 10 --warmup 3 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    kbench) step kbench 300 python tools/kernel_bench.py ;;
+    kprof) step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/kprof" -o kbench -- python3 tools/kernel_bench.py --reps 5 --rounds 1 ;;
+    pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv \
+             -d "$OUT/pmc" -o fetch -- python3 tools/kernel_bench.py --reps 3 --rounds 1 &&
+         step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$OUT/pmc" -o write -- python3 tools/kernel_bench.py --reps 3 --rounds 1 ;;
     speed) step speed 300 python -m rabit_amd.launcher -n 1 -- build/bin/speed_test 33554432 10 device=1 rabit_world1_fastpath=0 ;;
   esac
 done

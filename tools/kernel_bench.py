@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Bandwidth of the gfx950 data-plane kernels vs the HBM roof and vs PyTorch equivalents.
+
+Interleaved rounds in one process (A/B noise), random data, 128 MiB per operand by default.
+Bytes counted are the minimum each op must move: reduce2 3S, copy 2S, multi-k (k+1)S,
+prepare-dual 3S, checksum S.  Prints one JSON line per kernel.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from rabit_amd import ops  # noqa: E402
+
+HBM_ROOF_TBPS = 6.3  # measured float4 copy on MI355X (MI355X_MICROARCH.md)
+
+
+def timeit(fn, reps):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        start.record()
+        fn()
+        end.record()
+        end.synchronize()
+        times.append(start.elapsed_time(end) * 1e-3)
+    times.sort()
+    return times[len(times) // 2], times[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    n = args.mb * (1 << 20) // 4
+    S = n * 4
+    g = torch.Generator(device=dev).manual_seed(0)
+    a = torch.rand(n, generator=g, device=dev)
+    b = torch.rand(n, generator=g, device=dev)
+    out = torch.empty_like(a)
+    out2 = torch.empty_like(a)
+    srcs = [torch.rand(n // 4, generator=g, device=dev) for _ in range(8)]
+    out_small = torch.empty(n // 4, device=dev)
+    ai = torch.randint(0, 1 << 30, (n,), generator=g, device=dev, dtype=torch.int32)
+    bi = torch.randint(0, 1 << 30, (n,), generator=g, device=dev, dtype=torch.int32)
+    cases = {
+        "rabit_reduce_sum_f32": (lambda: ops.reduce_(a, b, ops.SUM), 3 * S),
+        "torch_add_f32": (lambda: a.add_(b), 3 * S),
+        "rabit_reduce_max_f32": (lambda: ops.reduce_(a, b, ops.MAX), 3 * S),
+        "rabit_reduce_bitor_i32": (lambda: ops.reduce_(ai, bi, ops.BITOR), 3 * S),
+        "torch_bitwise_or_i32": (lambda: ai.bitwise_or_(bi), 3 * S),
+        "rabit_copy": (lambda: ops.copy(out, a), 2 * S),
+        "rabit_prepare_copy": (lambda: ops.prepare(out, a, ops.PREP_COPY), 2 * S),
+        "torch_copy": (lambda: out.copy_(a), 2 * S),
+        "rabit_prepare_square_dual": (lambda: ops.prepare(out, a, ops.PREP_SQUARE, dst2=out2), 3 * S),
+        "torch_square_two_outputs": (lambda: (torch.mul(a, a, out=out), out2.copy_(out)), 4 * S),
+        "rabit_multi8_sum_f32": (lambda: ops.reduce_multi(out_small, srcs, ops.SUM), 9 * S // 4),
+        "torch_stack_sum8_f32": (lambda: torch.sum(torch.stack(srcs), dim=0, out=out_small),
+                                 9 * S // 4),
+        "rabit_checksum": (lambda: ops.checksum(a), S),
+    }
+    results = {k: [] for k in cases}
+    for _ in range(args.rounds):
+        for name, (fn, nbytes) in cases.items():
+            med, best = timeit(fn, args.reps)
+            results[name].append((med, best, nbytes))
+    for name, vals in results.items():
+        med = sorted(v[0] for v in vals)[len(vals) // 2]
+        best = min(v[1] for v in vals)
+        nbytes = vals[0][2]
+        rec = {"kernel": name, "mib_per_operand": args.mb, "median_us": round(med * 1e6, 1),
+               "best_us": round(best * 1e6, 1), "GBps": round(nbytes / med / 1e9, 1),
+               "pct_hbm_roof": round(100 * nbytes / med / 1e12 / HBM_ROOF_TBPS, 1)}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
