@@ -71,6 +71,16 @@ RABIT_DLL int RabitIsDevicePointer(const void *ptr);
 RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t count,
                                          int enum_dtype, int enum_op, int prep_op,
                                          double alpha);
+/*!
+ * \brief checkpoint n HBM buffers plus a host metadata blob: HBM snapshot + asynchronous
+ *        pinned-host mirror, registered as a lazy global checkpoint (version += 1)
+ */
+RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                                  const char *meta, rbt_ulong meta_len);
+/*! \brief load the latest device checkpoint into n HBM buffers; returns the version (0: none)
+ *         and the metadata blob (valid until the next call from this thread) */
+RABIT_DLL int RabitDevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                                     char **out_meta, rbt_ulong *out_meta_len);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

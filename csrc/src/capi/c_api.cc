@@ -223,6 +223,31 @@ RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t coun
   });
 }
 
+RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                                  const char *meta, rbt_ulong meta_len) {
+  GuardVoid([&]() {
+    rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+    rabit::utils::Check(e != nullptr, "device checkpoint needs a tracker-backed engine");
+    e->DevCheckPoint(n, ptrs, nbytes, std::string(meta == nullptr ? "" : meta, meta_len));
+  });
+}
+
+RABIT_DLL int RabitDevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                                     char **out_meta, rbt_ulong *out_meta_len) {
+  static thread_local std::string meta;
+  return Guard(
+      [&]() {
+        rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+        rabit::utils::Check(e != nullptr, "device checkpoint needs a tracker-backed engine");
+        meta.clear();
+        const int v = e->DevLoadCheckPoint(n, ptrs, nbytes, &meta);
+        *out_meta = rabit::BeginPtr(meta);
+        *out_meta_len = static_cast<rbt_ulong>(meta.size());
+        return v;
+      },
+      -1);
+}
+
 RABIT_DLL const char *RabitGetLastError() { return g_last_error.c_str(); }
 
 RABIT_DLL const char *RabitGetStats() {

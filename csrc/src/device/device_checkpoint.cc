@@ -1,0 +1,143 @@
+/*!
+ * \file device_checkpoint.cc
+ * \brief HBM snapshot checkpoints (see device_checkpoint.h).
+ */
+#include "device/device_checkpoint.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "device/kernels.h"
+#include "rabit/internal/utils.h"
+
+namespace rabit {
+namespace device {
+
+DeviceCheckpoint::DeviceCheckpoint(DevicePlane *plane) : plane_(plane) {
+  CheckHip(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(ckpt)");
+  CheckHip(hipEventCreateWithFlags(&snap_done_, hipEventDisableTiming), "hipEventCreate");
+  for (auto &h : half_) {
+    h.owner = this;
+    CheckHip(hipEventCreateWithFlags(&h.d2h_done, hipEventDisableTiming), "hipEventCreate");
+  }
+  loader_.owner = this;
+}
+
+DeviceCheckpoint::~DeviceCheckpoint() {
+  (void)hipStreamSynchronize(side_);
+  for (auto &h : half_) {
+    for (void *p : h.dev) (void)hipFree(p);
+    if (h.pinned != nullptr) (void)hipHostFree(h.pinned);
+    (void)hipEventDestroy(h.d2h_done);
+  }
+  (void)hipEventDestroy(snap_done_);
+  (void)hipStreamDestroy(side_);
+}
+
+size_t DeviceCheckpoint::reserved_bytes() const {
+  size_t s = 0;
+  for (const auto &h : half_) {
+    for (size_t c : h.cap) s += c;
+  }
+  return s;
+}
+
+const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const size_t *nbytes,
+                                               const std::string &meta) {
+  cur_ = 1 - cur_;
+  Half &h = half_[cur_];
+  // the previous D2H of this half must be done before its buffers are reused
+  CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
+  h.dev.resize(n, nullptr);
+  h.cap.resize(n, 0);
+  h.sizes.assign(nbytes, nbytes + n);
+  h.meta = meta;
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (h.cap[i] < nbytes[i]) {
+      if (h.dev[i] != nullptr) (void)hipFree(h.dev[i]);
+      CheckHip(hipMalloc(&h.dev[i], std::max<size_t>(nbytes[i], 256)), "hipMalloc(snapshot)");
+      h.cap[i] = std::max<size_t>(nbytes[i], 256);
+    }
+    total += nbytes[i];
+  }
+  if (h.pinned_cap < total) {
+    if (h.pinned != nullptr) (void)hipHostFree(h.pinned);
+    CheckHip(hipHostMalloc(reinterpret_cast<void **>(&h.pinned), std::max<size_t>(total, 1)),
+             "hipHostMalloc(mirror)");
+    h.pinned_cap = std::max<size_t>(total, 1);
+  }
+  // 1. HBM snapshot on the plane stream, ordered after the caller's stream
+  plane_->EnterFromUser();
+  for (int i = 0; i < n; ++i) plane_->CopyDeviceAsync(h.dev[i], ptrs[i], nbytes[i]);
+  CheckHip(hipEventRecord(snap_done_, plane_->stream()), "hipEventRecord(snapshot)");
+  // the caller may overwrite its tensors only after the snapshot read them
+  plane_->Finish(FailureProbe(), false);
+  // 2. pinned host mirror on the side stream
+  CheckHip(hipStreamWaitEvent(side_, snap_done_, 0), "hipStreamWaitEvent(mirror)");
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (nbytes[i] != 0) {
+      CheckHip(hipMemcpyAsync(h.pinned + off, h.dev[i], nbytes[i], hipMemcpyDeviceToHost, side_),
+               "D2H mirror");
+    }
+    off += nbytes[i];
+  }
+  CheckHip(hipEventRecord(h.d2h_done, side_), "hipEventRecord(mirror)");
+  return &h;
+}
+
+void DeviceCheckpoint::Half::Save(Stream *fo) const {
+  CheckHip(hipEventSynchronize(d2h_done), "checkpoint mirror wait");
+  uint64_t ml = meta.size();
+  fo->Write(&ml, sizeof(ml));
+  if (ml != 0) fo->Write(meta.data(), ml);
+  uint64_t n = sizes.size();
+  fo->Write(&n, sizeof(n));
+  for (size_t s : sizes) {
+    uint64_t v = s;
+    fo->Write(&v, sizeof(v));
+  }
+  size_t total = 0;
+  for (size_t s : sizes) total += s;
+  if (total != 0) fo->Write(pinned, total);
+}
+
+void DeviceCheckpoint::Half::Load(Stream *) { utils::Error("snapshot halves are save-only"); }
+
+Serializable *DeviceCheckpoint::Loader(int n, void *const *ptrs, const size_t *nbytes) {
+  loader_.ptrs.assign(ptrs, ptrs + n);
+  loader_.nbytes.assign(nbytes, nbytes + n);
+  loaded_meta_.clear();
+  return &loader_;
+}
+
+void DeviceCheckpoint::LoaderImpl::Load(Stream *fi) {
+  uint64_t ml = 0;
+  utils::Check(fi->Read(&ml, sizeof(ml)) == sizeof(ml), "device checkpoint: meta length");
+  owner->loaded_meta_.resize(ml);
+  if (ml != 0) {
+    utils::Check(fi->Read(&owner->loaded_meta_[0], ml) == ml, "device checkpoint: meta");
+  }
+  uint64_t n = 0;
+  utils::Check(fi->Read(&n, sizeof(n)) == sizeof(n), "device checkpoint: count");
+  utils::Check(n == ptrs.size(), "device checkpoint holds %llu buffers, %zu given",
+               static_cast<unsigned long long>(n), ptrs.size());
+  std::vector<uint64_t> sizes(n);
+  for (auto &s : sizes) utils::Check(fi->Read(&s, sizeof(s)) == sizeof(s), "device checkpoint: size");
+  std::vector<char> host;
+  for (size_t i = 0; i < n; ++i) {
+    utils::Check(sizes[i] == nbytes[i], "device checkpoint buffer %zu: %llu bytes stored, %zu given",
+                 i, static_cast<unsigned long long>(sizes[i]), nbytes[i]);
+    host.resize(sizes[i]);
+    if (sizes[i] == 0) continue;
+    utils::Check(fi->Read(host.data(), sizes[i]) == sizes[i], "device checkpoint: payload");
+    owner->plane_->StageToDevice(ptrs[i], host.data(), sizes[i]);
+  }
+}
+
+void DeviceCheckpoint::LoaderImpl::Save(Stream *) const {
+  utils::Error("the checkpoint loader is load-only");
+}
+}  // namespace device
+}  // namespace rabit

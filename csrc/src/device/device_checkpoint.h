@@ -1,0 +1,79 @@
+/*!
+ * \file device_checkpoint.h
+ * \brief Checkpoints of HBM-resident model state (SURVEY §5.4 MI355X plan).
+ *
+ * The reference serialises the global model into a host string at every CheckPoint.  For
+ * device tensors that means a synchronous D2H of the whole model on the critical path.  Here
+ * a checkpoint is:
+ *   1. an HBM-to-HBM snapshot of the tensors (gfx950 copy kernel, ~6 TB/s) into one of two
+ *      snapshot halves (double buffered: the previous version must stay intact until the new
+ *      checkpoint is acknowledged, peers may still be loading it),
+ *   2. an asynchronous D2H copy of the snapshot into pinned host memory on a side stream
+ *      (overlaps the next iteration; host-DRAM durability),
+ *   3. registration with the robust engine as a *lazy* checkpoint: bytes are produced (from the
+ *      pinned mirror, after its event) only if a recovering peer requests them.
+ * Wire format of the global checkpoint: uint64 meta_len, meta, uint64 n, n x uint64 size,
+ * then the n payloads.
+ */
+#ifndef XRABIT_DEVICE_DEVICE_CHECKPOINT_H_
+#define XRABIT_DEVICE_DEVICE_CHECKPOINT_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+#include <vector>
+
+#include "device/device_plane.h"
+#include "rabit/serializable.h"
+
+namespace rabit {
+namespace device {
+
+class DeviceCheckpoint {
+ public:
+  explicit DeviceCheckpoint(DevicePlane *plane);
+  ~DeviceCheckpoint();
+  /*!
+   * \brief snapshot n HBM buffers plus a host metadata blob into the next half and start its
+   *        D2H mirror; returns the Serializable to register as the (lazy) global checkpoint
+   */
+  const Serializable *Snapshot(int n, void *const *ptrs, const size_t *nbytes,
+                               const std::string &meta);
+  /*! \brief Serializable that loads a checkpoint into the given HBM buffers */
+  Serializable *Loader(int n, void *const *ptrs, const size_t *nbytes);
+  /*! \brief metadata of the last Load */
+  const std::string &loaded_meta() const { return loaded_meta_; }
+  /*! \brief bytes of HBM reserved by the two snapshot halves */
+  size_t reserved_bytes() const;
+
+ private:
+  struct Half : public Serializable {
+    DeviceCheckpoint *owner{nullptr};
+    std::vector<void *> dev;      // HBM snapshot buffers
+    std::vector<size_t> cap;      // their capacities
+    std::vector<size_t> sizes;    // payload sizes of the current snapshot
+    std::string meta;
+    char *pinned{nullptr};        // pinned host mirror
+    size_t pinned_cap{0};
+    hipEvent_t d2h_done{nullptr};
+    void Load(Stream *) override;
+    void Save(Stream *fo) const override;
+  };
+  struct LoaderImpl : public Serializable {
+    DeviceCheckpoint *owner{nullptr};
+    std::vector<void *> ptrs;
+    std::vector<size_t> nbytes;
+    void Load(Stream *fi) override;
+    void Save(Stream *) const override;
+  };
+  DevicePlane *plane_;
+  hipStream_t side_{nullptr};
+  hipEvent_t snap_done_{nullptr};
+  Half half_[2];
+  int cur_{1};
+  LoaderImpl loader_;
+  std::string loaded_meta_;
+};
+}  // namespace device
+}  // namespace rabit
+#endif  // XRABIT_DEVICE_DEVICE_CHECKPOINT_H_

@@ -127,6 +127,7 @@ bool EngineBase::Shutdown() {
   try {
     if (dev_) {
       dev_->Synchronize();
+      dev_ckpt_.reset();
       dev_.reset();
     }
     topo_.CloseAll();
@@ -367,6 +368,27 @@ void EngineBase::Allgather(void *buf, size_t total, size_t begin, size_t end, si
 }
 
 int EngineBase::LoadCheckPoint(Serializable *, Serializable *) { return 0; }
+
+void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                               const std::string &meta) {
+  utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
+  for (int i = 0; i < n; ++i) {
+    utils::Check(nbytes[i] == 0 || OnDevice(ptrs[i]), "device checkpoint: buffer %d not in HBM", i);
+  }
+  if (!dev_ckpt_) dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+  trace::Scope ts("device_snapshot", rank_, version_number_, seq_counter_, 0, 1);
+  const Serializable *snap = dev_ckpt_->Snapshot(n, ptrs, nbytes, meta);
+  this->LazyCheckPoint(snap);
+}
+
+int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
+                                  std::string *meta) {
+  utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
+  if (!dev_ckpt_) dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+  const int version = this->LoadCheckPoint(dev_ckpt_->Loader(n, ptrs, nbytes), nullptr);
+  if (version > 0 && meta != nullptr) *meta = dev_ckpt_->loaded_meta();
+  return version;
+}
 
 void EngineBase::CheckPoint(const Serializable *, const Serializable *) {
   version_number_ += 1;

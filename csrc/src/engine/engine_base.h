@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "coll/host_coll.h"
+#include "device/device_checkpoint.h"
 #include "device/device_plane.h"
 #include "net/links.h"
 #include "net/tracker_client.h"
@@ -82,6 +83,13 @@ class EngineBase : public IEngine {
   virtual void DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype, int op,
                                     int prep, double alpha, const char *_file, const int _line,
                                     const char *_caller);
+  /*!
+   * \brief checkpoint HBM buffers: HBM snapshot + async pinned mirror, registered as a lazy
+   *        global checkpoint (see device/device_checkpoint.h)
+   */
+  void DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes, const std::string &meta);
+  /*! \brief load the latest device checkpoint into HBM buffers; returns the version */
+  int DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes, std::string *meta);
   /*! \brief engine statistics as JSON */
   virtual std::string StatsJson() const;
   device::DevicePlane *device_plane() { return dev_.get(); }
@@ -141,6 +149,7 @@ class EngineBase : public IEngine {
   net::Topology topo_;
   std::unique_ptr<coll::HostCollectives> host_;
   std::unique_ptr<device::DevicePlane> dev_;
+  std::unique_ptr<device::DeviceCheckpoint> dev_ckpt_;
   void *user_stream_{nullptr};
   std::atomic<bool> abort_flag_{false};
   int rank_{0};

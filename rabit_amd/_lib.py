@@ -70,6 +70,12 @@ def _declare(d: ctypes.CDLL) -> None:
         "RabitDevAllreducePrepared": (None, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_int,
                                              c_double]),
         "RabitSetErrorMode": (None, [c_int]),
+        "RabitDevCheckPoint": (None, [c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t),
+                                      c_char_p, c_ulong]),
+        "RabitDevLoadCheckPoint": (c_int, [c_int, ctypes.POINTER(c_void_p),
+                                           ctypes.POINTER(c_size_t),
+                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_char)),
+                                           ctypes.POINTER(c_ulong)]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),
         "RabitTraceDump": (c_int, [c_char_p]),

@@ -313,6 +313,44 @@ def lazy_checkpoint(global_model: Any):
     _LIB.RabitLazyCheckPoint(_lazy_keep, len(_lazy_keep))
 
 
+def _tensor_list(tensors):
+    items = list(tensors.values()) if isinstance(tensors, dict) else list(tensors)
+    for t in items:
+        if not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
+            raise TypeError("device checkpoints take contiguous HBM (cuda) tensors")
+    n = len(items)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in items])
+    sizes = (ctypes.c_size_t * n)(*[t.numel() * t.element_size() for t in items])
+    return items, n, ptrs, sizes
+
+
+def checkpoint_tensors(tensors, meta: Any = None):
+    """Checkpoint HBM tensors (dict or list) plus a picklable `meta`: HBM snapshot with the
+    gfx950 copy kernel and an asynchronous pinned-host mirror on a side stream; the bytes are
+    only serialised if a recovering peer asks for them.  Version number += 1."""
+    _check_init()
+    items, n, ptrs, sizes = _tensor_list(tensors)
+    if items:
+        _sync_stream_for(items[0])
+    m = pickle.dumps(meta)
+    _LIB.RabitDevCheckPoint(n, ptrs, sizes, m, len(m))
+
+
+def load_checkpoint_tensors(tensors):
+    """Fill HBM tensors (same order/shapes as checkpointed) from the latest device
+    checkpoint; returns (version, meta), version 0 = nothing checkpointed (tensors untouched)."""
+    _check_init()
+    items, n, ptrs, sizes = _tensor_list(tensors)
+    if items:
+        _sync_stream_for(items[0])
+    mptr = ctypes.POINTER(ctypes.c_char)()
+    mlen = ctypes.c_ulong()
+    version = _LIB.RabitDevLoadCheckPoint(n, ptrs, sizes, ctypes.byref(mptr), ctypes.byref(mlen))
+    if version <= 0:
+        return (version, None)
+    return (version, _load_model(mptr, mlen.value))
+
+
 def version_number() -> int:
     _check_init()
     return _LIB.RabitVersionNumber()
