@@ -25,11 +25,11 @@ HIPFLAGS  := $(OPT) -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics 
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
 
 CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc \
-             csrc/src/coll/host_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc \
+             csrc/src/coll/host_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc csrc/src/device/peer_coll.cc \
              csrc/src/engine/engine_base.cc csrc/src/engine/engine_robust.cc \
              csrc/src/engine/recovery.cc csrc/src/capi/c_api.cc
 CORE_OBJS := $(patsubst csrc/src/%.cc,$(OBJ)/%.o,$(CORE_SRCS))
-KERN_OBJ  := $(OBJ)/device/kernels.o
+KERN_OBJ  := $(OBJ)/device/kernels.o $(OBJ)/device/peer_kernels.o
 HEADERS   := $(shell find csrc -name '*.h')
 
 FLAVOURS  := rabit rabit_base rabit_mock rabit_empty
@@ -43,7 +43,7 @@ $(OBJ)/%.o: csrc/src/%.cc $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(KERN_OBJ): csrc/src/device/kernels.hip csrc/src/device/kernels.h
+$(OBJ)/device/%.o: csrc/src/device/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -154,6 +154,7 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
 
 DevicePlane::~DevicePlane() {
   if (stream_ != nullptr) (void)hipStreamSynchronize(stream_);
+  peers_.reset();
   if (comm_ != nullptr) {
     ncclCommDestroy(comm_);
     comm_ = nullptr;
@@ -200,14 +201,59 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
   }
   nranks_ = nranks;
   rank_ = rank;
-  ++epoch_;
   return Status::kSuccess;
 }
 
 void DevicePlane::AbortComm() {
+  if (peers_ != nullptr) {
+    peers_->SignalAbort();  // spinning barriers give up; later kernels of the group are guarded
+  }
   if (comm_ != nullptr) {
     ncclCommAbort(comm_);
     comm_ = nullptr;
+  }
+  if (peers_ != nullptr) {
+    (void)hipStreamSynchronize(stream_);
+    peers_.reset();
+  }
+}
+
+void DevicePlane::DescribeDevice(PeerRecord *rec) const {
+  (void)hipDeviceGetPCIBusId(rec->pci, sizeof(rec->pci), device_);
+  gethostname(rec->host, sizeof(rec->host) - 1);
+  rec->device = device_;
+  rec->pid = static_cast<int32_t>(getpid());
+}
+
+bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
+  DropPeers();
+  try {
+    peers_.reset(new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_));
+  } catch (const std::exception &e) {
+    peers_.reset();
+    *why = e.what();
+    return false;
+  }
+  *rec = peers_->local();
+  return true;
+}
+
+bool DevicePlane::OpenPeers(const std::vector<PeerRecord> &all, int rank, std::string *why) {
+  if (peers_ == nullptr) {
+    *why = "no local peer buffers";
+    return false;
+  }
+  if (!peers_->Open(all, rank, why)) {
+    peers_.reset();
+    return false;
+  }
+  return true;
+}
+
+void DevicePlane::DropPeers() {
+  if (peers_ != nullptr) {
+    (void)hipStreamSynchronize(stream_);
+    peers_.reset();
   }
 }
 
@@ -222,7 +268,18 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
   const auto t0 = clock::now();
   for (uint64_t iter = 0;; ++iter) {
     hipError_t e = hipEventQuery(ev);
-    if (e == hipSuccess) return Status::kSuccess;
+    if (e == hipSuccess) {
+      if (peers_ != nullptr && peers_->failed()) {
+        utils::HandleLogInfo("[xrabit] direct transport: a peer barrier gave up\n");
+        if (force_ == 1) {
+          DropPeers();  // calibration probe: keep the RCCL communicator
+        } else {
+          AbortComm();
+        }
+        return Status::kAborted;
+      }
+      return Status::kSuccess;
+    }
     if (e != hipErrorNotReady) CheckHip(e, "device collective");
     if (comm_ != nullptr && (iter & 15) == 0) {
       ncclResult_t ae = ncclSuccess;
@@ -253,11 +310,19 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
 
 Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
   CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
+  Status s = Status::kSuccess;
+  if (cfg_.sync && host_wait) s = WaitEvent(ev_done_, probe);
+  if (pending_dst_ != nullptr) {
+    if (s == Status::kSuccess) {
+      CopyDeviceAsync(pending_dst_, pending_src_, pending_bytes_);
+      CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
+    }
+    pending_dst_ = nullptr;
+  }
   if (user_stream_ != stream_) {
     CheckHip(hipStreamWaitEvent(user_stream_, ev_done_, 0), "hipStreamWaitEvent(user)");
   }
-  if (!cfg_.sync || !host_wait) return Status::kSuccess;
-  return WaitEvent(ev_done_, probe);
+  return s;
 }
 
 void DevicePlane::Synchronize() { CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
@@ -294,14 +359,36 @@ void DevicePlane::StageToDevice(void *dev, const void *host, size_t bytes) {
   CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
-Status DevicePlane::Allreduce(const void *send, void *recv, size_t count, int dtype, int op,
-                              const FailureProbe &probe) {
+Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype,
+                              int op, int prep, double alpha, const FailureProbe &probe) {
+  const size_t bytes = count * TypeBytes(dtype);
+  if (UseDirect(bytes)) {
+    CheckHip(peers_->Allreduce(send, recv, recv2, count, dtype, op, prep, alpha),
+             "direct allreduce");
+    return Status::kSuccess;
+  }
   utils::Check(comm_ != nullptr, "device allreduce without communicator");
   ncclDataType_t t;
   ncclRedOp_t o;
   if (!RcclType(dtype, &t)) utils::Error("unsupported dtype %d on device", dtype);
-  if (!RcclOp(op, &o)) return AllreduceByKernel(send, recv, count, dtype, op, probe);
-  CheckNccl(ncclAllReduce(send, recv, count, t, o, comm_, stream_), "ncclAllReduce");
+  if (prep != kPrepCopy) {
+    CheckHip(LaunchPrepare(recv, nullptr, send, count, dtype, prep, alpha, stream_),
+             "LaunchPrepare");
+    send = recv;
+  }
+  if (!RcclOp(op, &o)) {
+    Status s = AllreduceByKernel(send, recv, count, dtype, op, probe);
+    if (s != Status::kSuccess) return s;
+  } else {
+    CheckNccl(ncclAllReduce(send, recv, count, t, o, comm_, stream_), "ncclAllReduce");
+  }
+  // RCCL writes recv only; the second copy is enqueued by Finish once the op is known to have
+  // succeeded (an aborted RCCL kernel leaves garbage in recv)
+  if (recv2 != nullptr && recv2 != recv) {
+    pending_dst_ = recv2;
+    pending_src_ = recv;
+    pending_bytes_ = bytes;
+  }
   return Status::kSuccess;
 }
 
@@ -359,6 +446,10 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
 
 Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe) {
   (void)probe;
+  if (UseDirect(bytes)) {
+    CheckHip(peers_->Broadcast(buf, bytes, root), "direct broadcast");
+    return Status::kSuccess;
+  }
   utils::Check(comm_ != nullptr, "device broadcast without communicator");
   CheckNccl(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
   return Status::kSuccess;
@@ -367,6 +458,10 @@ Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailurePr
 Status DevicePlane::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
                                const std::vector<size_t> &size, const FailureProbe &probe) {
   (void)probe;
+  if (UseDirect(total)) {
+    CheckHip(peers_->AllgatherV(buf_, total, begin, size), "direct allgather");
+    return Status::kSuccess;
+  }
   utils::Check(comm_ != nullptr, "device allgather without communicator");
   char *buf = static_cast<char *>(buf_);
   const int n = nranks_;

@@ -21,9 +21,11 @@
 #include <rccl/rccl.h>
 
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "device/peer_coll.h"
 #include "net/socket.h"
 
 namespace rabit {
@@ -41,6 +43,10 @@ struct DeviceConfig {
   size_t arena_chunk{256u << 20};      // result-log arena growth step
   size_t arena_cap{size_t(64) << 30};  // beyond this the result log falls back to host memory
   int spin_us{5000};                   // busy-poll window before sleeping while waiting
+  int algo{0};                         // 0 auto, 1 RCCL only, 2 direct (IPC peer memory) only
+  size_t peer_stage{256u << 20};       // direct transport: bytes per stage buffer (x2 per rank)
+  double peer_deadline_sec{120};       // direct transport: barrier gives up after this long
+  size_t direct_min_bytes{1u << 20};   // auto: ops of at least this size use the direct path
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -89,15 +95,51 @@ class DevicePlane {
   static std::string NewUniqueId();
   /*! \brief collective over all ranks: build the communicator of a new epoch */
   Status InitComm(const std::string &id, int nranks, int rank, const FailureProbe &probe);
-  /*! \brief abort the communicator (unblocks in-flight kernels), drop it */
+  /*! \brief abort the communicator and the peer group (unblocks in-flight kernels), drop them */
   void AbortComm();
   bool has_comm() const { return comm_ != nullptr; }
+  bool has_peers() const { return peers_ != nullptr; }
+  /*! \brief a transport for world > 1 is up */
+  bool ready() const { return comm_ != nullptr || peers_ != nullptr; }
   int epoch() const { return epoch_; }
+  /*! \brief count a new communicator epoch (after InitComm and/or OpenPeers) */
+  void BeginEpoch(int nranks, int rank) {
+    nranks_ = nranks;
+    rank_ = rank;
+    ++epoch_;
+  }
+
+  // ---- direct transport (IPC peer memory over xGMI)
+  /*! \brief allocate and export the local stage buffers; false (with why) if impossible */
+  bool PreparePeers(PeerRecord *rec, std::string *why);
+  /*! \brief map every rank's buffers (records in rank order) */
+  bool OpenPeers(const std::vector<PeerRecord> &all, int rank, std::string *why);
+  void DropPeers();
+  /*! \brief route an op of this many bytes over the direct transport */
+  bool UseDirect(size_t bytes) const {
+    if (peers_ == nullptr) return false;
+    if (force_ >= 0) return force_ == 1;
+    return comm_ == nullptr || cfg_.algo == 2 || bytes >= cfg_.direct_min_bytes;
+  }
+  void set_direct_min_bytes(size_t b) { cfg_.direct_min_bytes = b; }
+  size_t direct_min_bytes() const { return cfg_.direct_min_bytes; }
+  /*! \brief calibration: -1 normal routing, 0 force RCCL, 1 force direct */
+  void ForceTransport(int which) { force_ = which; }
+  /*! \brief barrier deadline of the direct transport (calibration runs with a short one) */
+  void SetPeerDeadline(double sec) {
+    if (peers_ != nullptr) peers_->set_deadline_sec(sec);
+  }
+  /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
+  void DescribeDevice(PeerRecord *rec) const;
 
   // ---- collectives (enqueue then wait)
-  /*! \brief recv = reduce(send) over ranks; send may equal recv */
-  Status Allreduce(const void *send, void *recv, size_t count, int dtype, int op,
-                   const FailureProbe &probe);
+  /*!
+   * \brief recv = reduce(prep(send)) over ranks, also stored to recv2 when given; send may equal
+   *        recv.  prep is a PrepOp (kPrepCopy: none).  recv2 is written only when the op
+   *        succeeds on this rank, so a retry still finds the input.
+   */
+  Status Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
+                   int prep, double alpha, const FailureProbe &probe);
   Status Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe);
   /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place */
   Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
@@ -133,6 +175,11 @@ class DevicePlane {
   ncclComm_t comm_{nullptr};
   int nranks_{0}, rank_{0}, epoch_{0};
   DeviceArena arena_;
+  std::unique_ptr<PeerGroup> peers_;
+  int force_{-1};
+  void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
+  const void *pending_src_{nullptr};
+  size_t pending_bytes_{0};
   void *scratch_[2]{nullptr, nullptr};
   size_t scratch_bytes_[2]{0, 0};
   void *pinned_{nullptr};

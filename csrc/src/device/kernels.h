@@ -26,9 +26,13 @@ constexpr int kMaxReduceSources = 8;
 /*! \brief dst[i] = op(dst[i], src[i]) */
 hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int op,
                         hipStream_t stream);
-/*! \brief dst[i] = op(srcs[0][i], ..., srcs[nsrc-1][i]), 1 <= nsrc <= 8 (dst may alias srcs[0]) */
+/*!
+ * \brief dst[i] = op(srcs[0][i], ..., srcs[nsrc-1][i]), 1 <= nsrc <= 8 (dst may alias any
+ *        source).  guard: optional device word; the launch does nothing when it is non-zero
+ *        (set by a failed peer barrier earlier on the stream).
+ */
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
-                             int dtype, int op, hipStream_t stream);
+                             int dtype, int op, hipStream_t stream, const int *guard = nullptr);
 /*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);

@@ -136,10 +136,17 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
 // ---------------------------------------------------------------- multi-source reduce
 struct SrcList {
   const void *p[kMaxReduceSources];
+  const int *guard;  // optional: skip the whole launch when *guard != 0 (failed peer barrier)
 };
+
+__device__ __forceinline__ bool Guarded(const int *guard) {
+  return guard != nullptr &&
+         __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
 
 template <typename T, int OP, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList srcs, size_t n) {
+  if (Guarded(srcs.guard)) return;
   const size_t nvec = n * sizeof(T) / 16;
   const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
   uint4 *d = reinterpret_cast<uint4 *>(dst);
@@ -180,7 +187,7 @@ template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcList srcs, int nsrc,
                                                                   size_t n) {
   const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || Guarded(srcs.guard)) return;
   T acc = static_cast<const T *>(srcs.p[0])[i];
   for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
   dst[i] = acc;
@@ -195,8 +202,10 @@ void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
 }
 
 template <typename T, int OP>
-hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st,
+                       const int *guard) {
   SrcList sl;
+  sl.guard = guard;
   bool aligned = Aligned16(dst);
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;
@@ -443,8 +452,9 @@ struct OrTag {
     if constexpr (std::is_integral<T>::value) return Reduce2<T, kOpOr>(d, s, n, st);
     return hipErrorInvalidValue;
   }
-  static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st) {
-    if constexpr (std::is_integral<T>::value) return ReduceMulti<T, kOpOr>(d, s, k, n, st);
+  static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st,
+                            const int *guard) {
+    if constexpr (std::is_integral<T>::value) return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard);
     return hipErrorInvalidValue;
   }
 };
@@ -466,16 +476,16 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 }
 
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
-                             int dtype, int op, hipStream_t stream) {
+                             int dtype, int op, hipStream_t stream, const int *guard) {
   if (count == 0) return hipSuccess;
   if (nsrc < 1 || nsrc > kMaxReduceSources) return hipErrorInvalidValue;
   return DispatchType(dtype, op == kOpOr, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;
     switch (op) {
-      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream);
-      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream);
-      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream);
-      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream);
+      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard);
+      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard);
+      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard);
+      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard);
       default: return hipErrorInvalidValue;
     }
   });

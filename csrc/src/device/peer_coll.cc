@@ -1,0 +1,282 @@
+/*!
+ * \file peer_coll.cc
+ * \brief Host side of the direct (IPC peer-memory) transport; see peer_coll.h.
+ */
+#include "device/peer_coll.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "device/device_plane.h"
+#include "device/kernels.h"
+#include "rabit/internal/utils.h"
+
+namespace rabit {
+namespace device {
+namespace {
+size_t ElemBytes(int dtype) {
+  switch (dtype) {
+    case 0:
+    case 1: return 1;
+    case 2:
+    case 3:
+    case 6: return 4;
+    default: return 8;
+  }
+}
+
+inline size_t RoundUp(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+/*! \brief [lo, hi) of segment p when c items are cut into n segments of `seg` */
+inline void SegRange(size_t c, size_t seg, int p, size_t *lo, size_t *hi) {
+  *lo = std::min(c, seg * static_cast<size_t>(p));
+  *hi = std::min(c, *lo + seg);
+}
+
+void AddSeg(CopyBatch *b, char *dst, const char *src, char *dst2, size_t bytes) {
+  if (bytes == 0) return;
+  utils::Assert(b->n < kMaxCopySegs, "copy batch overflow");
+  b->seg[b->n++] = CopySeg{dst, src, dst2, bytes};
+}
+
+/*! \brief the (at most two) byte ranges of a wrapping slice [begin, begin+size) mod total */
+int SliceRanges(size_t begin, size_t size, size_t total, size_t lo[2], size_t hi[2]) {
+  if (size == 0) return 0;
+  begin %= total;
+  lo[0] = begin;
+  hi[0] = std::min(total, begin + size);
+  if (begin + size <= total) return 1;
+  lo[1] = 0;
+  hi[1] = begin + size - total;
+  return 2;
+}
+}  // namespace
+
+PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream)
+    : device_(device), stage_bytes_(RoundUp(std::max<size_t>(stage_bytes, 1 << 20), 1 << 16)),
+      stream_(stream) {
+  CheckHip(hipSetDevice(device_), "hipSetDevice");
+  void *p = nullptr;
+  // uncached: peers poll the flags and stream the stage buffers over xGMI; nothing of it may
+  // linger in a (non-coherent) L2 between ops
+  CheckHip(hipExtMallocWithFlags(&p, kPeerFlagBytes + 2 * stage_bytes_, hipDeviceMallocUncached),
+           "hipExtMallocWithFlags(peer stage)");
+  base_ = static_cast<char *>(p);
+  CheckHip(hipMemset(base_, 0, kPeerFlagBytes), "hipMemset(flags)");
+  CheckHip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hipIpcMemHandle_t h;
+  CheckHip(hipIpcGetMemHandle(&h, base_), "hipIpcGetMemHandle");
+  static_assert(sizeof(h) <= sizeof(local_.ipc), "ipc handle size");
+  std::memcpy(local_.ipc, &h, sizeof(h));
+  CheckHip(hipDeviceGetPCIBusId(local_.pci, sizeof(local_.pci), device_), "hipDeviceGetPCIBusId");
+  gethostname(local_.host, sizeof(local_.host) - 1);
+  local_.stage_bytes = stage_bytes_;
+  local_.pid = static_cast<int32_t>(getpid());
+  local_.device = device_;
+  void *hw = nullptr;
+  CheckHip(hipHostMalloc(&hw, 64, hipHostMallocCoherent | hipHostMallocMapped),
+           "hipHostMalloc(peer words)");
+  host_words_ = static_cast<int *>(hw);
+  std::memset(host_words_, 0, 64);
+  CheckHip(hipDeviceGetAttribute(&clock_khz_, hipDeviceAttributeWallClockRate, device_),
+           "wall clock");
+  set_deadline_sec(deadline_sec);
+}
+
+PeerGroup::~PeerGroup() {
+  (void)hipSetDevice(device_);
+  for (size_t r = 0; r < peer_base_.size(); ++r) {
+    if (peer_base_[r] != nullptr && peer_base_[r] != base_) (void)hipIpcCloseMemHandle(peer_base_[r]);
+  }
+  if (base_ != nullptr) (void)hipFree(base_);
+  if (host_words_ != nullptr) (void)hipHostFree(host_words_);
+}
+
+bool PeerGroup::Open(const std::vector<PeerRecord> &all, int rank, std::string *why) {
+  const int n = static_cast<int>(all.size());
+  if (n < 1 || n > kMaxPeers) {
+    *why = "group size " + std::to_string(n) + " not in [1, 8]";
+    return false;
+  }
+  for (int r = 0; r < n; ++r) {
+    if (std::strncmp(all[r].host, local_.host, sizeof(local_.host)) != 0) {
+      *why = std::string("rank ") + std::to_string(r) + " is on another host";
+      return false;
+    }
+    if (all[r].stage_bytes != stage_bytes_) {
+      *why = "stage sizes differ";
+      return false;
+    }
+  }
+  peer_base_.assign(n, nullptr);
+  for (int r = 0; r < n; ++r) {
+    if (r == rank) {
+      peer_base_[r] = base_;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, all[r].ipc, sizeof(h));
+    void *p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      *why = std::string("hipIpcOpenMemHandle(rank ") + std::to_string(r) +
+             "): " + hipGetErrorString(e);
+      return false;
+    }
+    peer_base_[r] = static_cast<char *>(p);
+  }
+  n_ = n;
+  rank_ = rank;
+  opened_ = true;
+  return true;
+}
+
+char *PeerGroup::stage(int rank, int which) const {
+  return peer_base_[rank] + kPeerFlagBytes + static_cast<size_t>(which) * stage_bytes_;
+}
+
+void PeerGroup::SignalAbort() {
+  if (host_words_ != nullptr) {
+    __atomic_store_n(&host_words_[0], 1, __ATOMIC_SEQ_CST);
+  }
+}
+
+bool PeerGroup::failed() const {
+  return host_words_ != nullptr && __atomic_load_n(&host_words_[1], __ATOMIC_SEQ_CST) != 0;
+}
+
+hipError_t PeerGroup::Barrier() {
+  PeerFlagTable t;
+  for (int p = 0; p < kMaxPeers; ++p) {
+    t.p[p] = p < n_ ? reinterpret_cast<unsigned long long *>(peer_base_[p]) : nullptr;
+  }
+  ++epoch_;
+  return LaunchPeerBarrier(t, rank_, n_, epoch_, &host_words_[0], dev_status(), &host_words_[1],
+                           deadline_ticks_, stream_);
+}
+
+#define XRABIT_TRY_HIP(expr)              \
+  do {                                    \
+    hipError_t e_ = (expr);               \
+    if (e_ != hipSuccess) return e_;      \
+  } while (0)
+
+hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_t count,
+                                int dtype, int op, int prep, double alpha) {
+  utils::Assert(opened_, "peer group not opened");
+  const size_t tn = ElemBytes(dtype);
+  const size_t quantum = 64 * static_cast<size_t>(n_);  // keeps segments 256-B aligned
+  const size_t chunk = std::max(quantum, (stage_bytes_ / tn) / quantum * quantum);
+  const char *in = static_cast<const char *>(send);
+  char *out = static_cast<char *>(recv);
+  char *out2 = static_cast<char *>(recv2);
+  for (size_t off = 0; off < count; off += chunk) {
+    const size_t c = std::min(chunk, count - off);
+    const int which = parity_;
+    parity_ ^= 1;
+    char *mine = stage(rank_, which);
+    if (prep == kPrepCopy) {
+      XRABIT_TRY_HIP(LaunchCopy(mine, in + off * tn, c * tn, stream_));
+    } else {
+      XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, in + off * tn, c, dtype, prep, alpha, stream_));
+    }
+    XRABIT_TRY_HIP(Barrier());
+    const size_t seg = RoundUp((c + n_ - 1) / n_, 64);
+    size_t lo, hi;
+    SegRange(c, seg, rank_, &lo, &hi);
+    if (hi > lo) {
+      const void *srcs[kMaxPeers];
+      for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which) + lo * tn;  // rank order: identical
+      XRABIT_TRY_HIP(
+          LaunchReduceMulti(mine + lo * tn, srcs, n_, hi - lo, dtype, op, stream_, dev_status()));
+    }
+    XRABIT_TRY_HIP(Barrier());
+    CopyBatch b;
+    NewBatch(&b);
+    for (int p = 0; p < n_; ++p) {
+      SegRange(c, seg, p, &lo, &hi);
+      const size_t at = (off + lo) * tn;
+      AddSeg(&b, out + at, stage(p, which) + lo * tn, out2 != nullptr ? out2 + at : nullptr,
+             (hi - lo) * tn);
+    }
+    XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+  }
+  return hipSuccess;
+}
+
+hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root) {
+  utils::Assert(opened_, "peer group not opened");
+  char *user = static_cast<char *>(buf);
+  for (size_t off = 0; off < bytes; off += stage_bytes_) {
+    const size_t c = std::min(stage_bytes_, bytes - off);
+    const int which = parity_;
+    parity_ ^= 1;
+    if (rank_ == root) XRABIT_TRY_HIP(LaunchCopy(stage(root, which), user + off, c, stream_));
+    XRABIT_TRY_HIP(Barrier());
+    const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
+    size_t lo, hi;
+    CopyBatch b;
+    NewBatch(&b);
+    if (rank_ != root) {
+      // scatter: pull my segment from the root (kept in my stage buffer for the others)
+      SegRange(c, seg, rank_, &lo, &hi);
+      AddSeg(&b, stage(rank_, which) + lo, stage(root, which) + lo, user + off + lo, hi - lo);
+      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    }
+    XRABIT_TRY_HIP(Barrier());
+    if (rank_ != root) {
+      NewBatch(&b);
+      for (int q = 0; q < n_; ++q) {
+        if (q == rank_) continue;
+        SegRange(c, seg, q, &lo, &hi);
+        AddSeg(&b, user + off + lo, stage(q, which) + lo, nullptr, hi - lo);
+      }
+      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
+                                 const std::vector<size_t> &size) {
+  utils::Assert(opened_, "peer group not opened");
+  char *user = static_cast<char *>(buf);
+  for (size_t wlo = 0; wlo < total; wlo += stage_bytes_) {
+    const size_t whi = std::min(total, wlo + stage_bytes_);
+    const int which = parity_;
+    parity_ ^= 1;
+    CopyBatch b;
+    NewBatch(&b);
+    for (int p = 0; p < n_; ++p) {
+      size_t lo[2], hi[2];
+      const int k = SliceRanges(begin[p], size[p], total, lo, hi);
+      for (int j = 0; j < k; ++j) {
+        const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
+        if (z <= a) continue;
+        if (p == rank_) {
+          AddSeg(&b, stage(rank_, which) + (a - wlo), user + a, nullptr, z - a);
+        }
+      }
+    }
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    XRABIT_TRY_HIP(Barrier());
+    NewBatch(&b);
+    for (int p = 0; p < n_; ++p) {
+      if (p == rank_) continue;
+      size_t lo[2], hi[2];
+      const int k = SliceRanges(begin[p], size[p], total, lo, hi);
+      for (int j = 0; j < k; ++j) {
+        const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
+        if (z > a) AddSeg(&b, user + a, stage(p, which) + (a - wlo), nullptr, z - a);
+      }
+    }
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+  }
+  return hipSuccess;
+}
+#undef XRABIT_TRY_HIP
+}  // namespace device
+}  // namespace rabit

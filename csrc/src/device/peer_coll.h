@@ -1,0 +1,139 @@
+/*!
+ * \file peer_coll.h
+ * \brief Direct transport of the device plane: collectives that read peer HBM through IPC
+ *        mappings (xGMI between the GPUs of one MI355X node).
+ *
+ * Every rank exports one uncached allocation [flags | stage 0 | stage 1] and maps its peers'.
+ * An op stages its input in the local stage buffer, meets the peers at a flag barrier, and then
+ * pulls what it needs from the peers' stage buffers with streaming kernels, so each of the 7
+ * xGMI links of a GPU carries 1/7 of the traffic at the same time (a ring uses one link per
+ * direction).  Stage buffers alternate between ops, which lets two barriers per allreduce
+ * suffice (SURVEY §5.8 "direct peer access with our own multi-source reduce kernel").
+ *
+ *  - Allreduce (two-shot): stage; barrier; rank r reduces segment r of all n stage buffers
+ *    in place with the multi-source kernel; barrier; everyone gathers the n reduced segments
+ *    (optionally storing them twice: result log + user buffer).  Per rank, 2(n-1)/n of the
+ *    payload crosses xGMI — the bandwidth-optimal amount — spread over all links.
+ *  - Broadcast: root stages; barrier; rank p pulls segment p from the root; barrier; everyone
+ *    pulls the other segments from their owners (scatter + allgather: the root's links carry
+ *    2/n of the payload each instead of all of it).
+ *  - AllgatherV (rabit's variable, wrapping slices): stage own slice; barrier; pull the rest.
+ *
+ * Ranks that share one GPU also work (IPC within a device), which is how the multi-rank device
+ * path is tested on a one-GPU machine.  Failure handling: the barrier gives up when the host
+ * raises the abort word or a deadline passes, and reports it in a status word; the owner then
+ * drops the whole group (epochs are not resynchronised, a new group is built).
+ */
+#ifndef XRABIT_DEVICE_PEER_COLL_H_
+#define XRABIT_DEVICE_PEER_COLL_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <algorithm>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace rabit {
+namespace device {
+
+constexpr int kMaxPeers = 8;
+constexpr int kMaxCopySegs = 16;
+/*! \brief bytes of the flag area at the start of each exported allocation: kMaxPeers arrival
+ *  flags at offset 0, the local failure word at kPeerStatusOffset */
+constexpr size_t kPeerFlagBytes = 64 * 1024;
+constexpr size_t kPeerStatusOffset = 4096;
+
+struct PeerFlagTable {
+  unsigned long long *p[kMaxPeers];
+};
+
+struct CopySeg {
+  char *dst;
+  const char *src;
+  char *dst2;  // optional second destination (nullptr: none)
+  size_t bytes;
+};
+
+struct CopyBatch {
+  CopySeg seg[kMaxCopySegs];
+  int n;
+  const int *guard;  // optional device word: the launch does nothing when it is non-zero
+};
+
+hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
+                             const volatile int *abort_word, int *dev_status, int *host_status,
+                             long long deadline_ticks, hipStream_t stream);
+hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream);
+
+/*! \brief fixed-size record every rank contributes when a group is built */
+struct PeerRecord {
+  char ipc[64];      // hipIpcMemHandle_t of the exported allocation
+  char pci[32];      // PCI bus id of the GPU
+  char host[64];     // host name
+  uint64_t stage_bytes;
+  int32_t pid;
+  int32_t device;
+};
+
+class PeerGroup {
+ public:
+  /*! \brief allocate and export the local buffers; stage_bytes per stage buffer */
+  PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream);
+  ~PeerGroup();
+  PeerGroup(const PeerGroup &) = delete;
+  PeerGroup &operator=(const PeerGroup &) = delete;
+
+  const PeerRecord &local() const { return local_; }
+  /*!
+   * \brief map every peer's allocation; all must be on this host with equal stage sizes.
+   * \return false (and an explanation in why) when the group cannot be built
+   */
+  bool Open(const std::vector<PeerRecord> &all, int rank, std::string *why);
+  int size() const { return n_; }
+  size_t stage_bytes() const { return stage_bytes_; }
+
+  // enqueue on the stream given at construction (the caller waits / checks status)
+  hipError_t Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
+                       int prep, double alpha);
+  hipError_t Broadcast(void *buf, size_t bytes, int root);
+  hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
+                        const std::vector<size_t> &size);
+
+  /*! \brief make spinning barriers give up (host side; safe at any time) */
+  void SignalAbort();
+  /*! \brief true when a barrier gave up (read after the stream drained) */
+  bool failed() const;
+  uint64_t barriers() const { return epoch_; }
+  void set_deadline_sec(double sec) {
+    deadline_ticks_ = static_cast<long long>(std::max(sec, 0.1) * clock_khz_ * 1000.0);
+  }
+
+ private:
+  hipError_t Barrier();
+  char *stage(int rank, int which) const;
+  int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
+  void NewBatch(CopyBatch *b) const {
+    b->n = 0;
+    b->guard = dev_status();
+  }
+
+  int device_;
+  size_t stage_bytes_;
+  hipStream_t stream_;
+  long long deadline_ticks_{0};
+  int clock_khz_{100000};
+  char *base_{nullptr};                 // local allocation
+  std::vector<char *> peer_base_;       // mapped allocations (own = base_)
+  int *host_words_{nullptr};            // pinned: [0] abort, [1] status
+  int n_{0}, rank_{0};
+  unsigned long long epoch_{0};
+  int parity_{0};
+  PeerRecord local_{};
+  bool opened_{false};
+};
+
+}  // namespace device
+}  // namespace rabit
+#endif  // XRABIT_DEVICE_PEER_COLL_H_

@@ -1,0 +1,138 @@
+/*!
+ * \file peer_kernels.hip
+ * \brief gfx950 kernels of the direct (IPC / xGMI peer-memory) transport: a cross-process
+ *        flag barrier and a batched multi-segment copy that pulls peer segments over xGMI.
+ *
+ * Barrier: every rank owns an array of one 64-bit flag per peer inside its IPC-exported,
+ * uncached staging allocation.  Arriving at barrier number e, rank r stores e into slot r of
+ * every peer's array (system-scope release) and then spins until all n slots of its own array
+ * are >= e (system-scope acquire).  Epochs only grow, so flags never need resetting.  Each lane
+ * polls with s_sleep back-off and gives up when the host raises the abort word (peer failure
+ * seen on the TCP control plane) or the wall-clock deadline passes — every wave reaches an exit.
+ * A failure is recorded in a device word (the guard every later kernel of the group checks
+ * first, so nothing is written after a failed barrier) and in a pinned host word.
+ *
+ * Copy batch: up to kMaxCopySegs (dst, src[, dst2]) segments in one launch; workgroup b takes
+ * tile b / nseg of segment b % nseg, so the workgroups in flight read from every peer at once
+ * and all xGMI links carry traffic together.  Tiles are 256 lanes x 4 x 16 B like the other
+ * streaming kernels (kernels.hip).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "device/peer_coll.h"
+
+namespace rabit {
+namespace device {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
+constexpr size_t kTileBytes = static_cast<size_t>(kBlock) * kUnroll * 16;
+
+__global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int rank, int n,
+                                                        unsigned long long epoch,
+                                                        const volatile int *abort_word,
+                                                        int *dev_status, int *host_status,
+                                                        long long deadline_ticks) {
+  const int t = threadIdx.x;
+  // an earlier barrier of this group failed: stay failed, signal nothing
+  if (__hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  // make the bytes written by earlier kernels of this stream visible before signalling
+  __threadfence_system();
+  if (t < n) {
+    __hip_atomic_store(flags.p[t] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long *mine = flags.p[rank] + t;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (*abort_word != 0 || wall_clock64() - t0 > deadline_ticks) {
+        __hip_atomic_store(dev_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  __threadfence_system();
+}
+
+__device__ __forceinline__ bool Al16(const void *p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+__global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
+  if (batch.guard != nullptr &&
+      __hip_atomic_load(batch.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    return;
+  }
+  const int s = static_cast<int>(blockIdx.x % static_cast<unsigned>(batch.n));
+  const size_t tile = blockIdx.x / static_cast<unsigned>(batch.n);
+  const CopySeg &g = batch.seg[s];
+  const size_t lo = tile * kTileBytes;
+  if (lo >= g.bytes) return;
+  const size_t hi = std::min(g.bytes, lo + kTileBytes);
+  const bool vec = Al16(g.dst) && Al16(g.src) && (g.dst2 == nullptr || Al16(g.dst2));
+  if (vec) {
+    const size_t nv = (hi - lo) / 16;  // lo is a multiple of 16
+    const uint4 *src = reinterpret_cast<const uint4 *>(g.src + lo);
+    uint4 *dst = reinterpret_cast<uint4 *>(g.dst + lo);
+    uint4 *dst2 = g.dst2 != nullptr ? reinterpret_cast<uint4 *>(g.dst2 + lo) : nullptr;
+    if (nv == static_cast<size_t>(kBlock) * kUnroll) {
+      uint4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = src[threadIdx.x + u * kBlock];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) dst[threadIdx.x + u * kBlock] = v[u];
+      if (dst2 != nullptr) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) dst2[threadIdx.x + u * kBlock] = v[u];
+      }
+    } else {
+      for (size_t i = threadIdx.x; i < nv; i += kBlock) {
+        const uint4 v = src[i];
+        dst[i] = v;
+        if (dst2 != nullptr) dst2[i] = v;
+      }
+      // trailing bytes of the segment (< 16)
+      for (size_t i = lo + nv * 16 + threadIdx.x; i < hi; i += kBlock) {
+        const char c = g.src[i];
+        g.dst[i] = c;
+        if (g.dst2 != nullptr) g.dst2[i] = c;
+      }
+    }
+  } else {
+    for (size_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+      const char c = g.src[i];
+      g.dst[i] = c;
+      if (g.dst2 != nullptr) g.dst2[i] = c;
+    }
+  }
+}
+}  // namespace
+
+hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
+                             const volatile int *abort_word, int *dev_status, int *host_status,
+                             long long deadline_ticks, hipStream_t stream) {
+  if (n < 1 || n > kMaxPeers || rank < 0 || rank >= n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(PeerBarrierKernel, dim3(1), dim3(64), 0, stream, flags, rank, n, epoch,
+                     abort_word, dev_status, host_status, deadline_ticks);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream) {
+  if (batch.n < 0 || batch.n > kMaxCopySegs) return hipErrorInvalidValue;
+  size_t tiles = 0;
+  for (int i = 0; i < batch.n; ++i) {
+    tiles = std::max(tiles, (batch.seg[i].bytes + kTileBytes - 1) / kTileBytes);
+  }
+  if (tiles == 0) return hipSuccess;
+  const size_t grid = tiles * static_cast<size_t>(batch.n);
+  if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(CopyBatchKernel, dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, stream,
+                     batch);
+  return hipGetLastError();
+}
+}  // namespace device
+}  // namespace rabit

@@ -67,6 +67,25 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_spin_us")) dcfg_.spin_us = atoi(val);
   if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
+  if (is("rabit_device_algo")) {
+    const std::string v(val);
+    if (v == "auto") {
+      dcfg_.algo = 0;
+    } else if (v == "rccl") {
+      dcfg_.algo = 1;
+    } else if (v == "direct") {
+      dcfg_.algo = 2;
+    } else {
+      utils::Error("rabit_device_algo must be auto, rccl or direct (got %s)", val);
+    }
+  }
+  if (is("rabit_device_peer_buffer")) dcfg_.peer_stage = core::ParseUnit(name, val);
+  if (is("rabit_device_peer_timeout_sec")) dcfg_.peer_deadline_sec = atof(val);
+  if (is("rabit_device_direct_min")) {
+    dcfg_.direct_min_bytes = core::ParseUnit(name, val);
+    calibrate_ = false;  // an explicit threshold wins over the measured one
+  }
+  if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
   if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
@@ -210,17 +229,158 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
 
 Status EngineBase::EnsureDeviceComm() {
   utils::Check(dev_ != nullptr, "device buffer given but the device plane is disabled");
-  if (dev_->has_comm()) return Status::kSuccess;
-  std::string id(sizeof(ncclUniqueId), '\0');
-  if (rank_ == 0) id = device::DevicePlane::NewUniqueId();
-  Status s = host_->TreeBroadcast(&id[0], id.size(), 0);
+  if (dev_->ready()) return Status::kSuccess;
+  const int n = GetWorldSize();
+  // 1. every rank describes its GPU (and exports its peer buffers when the direct transport
+  //    may be used); the records travel around the host ring
+  device::PeerRecord rec;
+  std::memset(&rec, 0, sizeof(rec));
+  std::string why;
+  bool have_peers = false;
+  if (dcfg_.algo != 1 && n <= device::kMaxPeers) {
+    have_peers = dev_->PreparePeers(&rec, &why);
+    if (!have_peers && debug_) {
+      utils::HandleLogInfo("[%d] direct transport unavailable: %s\n", rank_, why.c_str());
+    }
+  }
+  if (!have_peers) dev_->DescribeDevice(&rec);
+  const size_t rb = sizeof(rec);
+  std::vector<device::PeerRecord> all(n);
+  std::memcpy(&all[rank_], &rec, rb);
+  Status s = host_->RingAllgather(all.data(), rb * n, rb * rank_, rb * (rank_ + 1), rb);
   if (s != Status::kSuccess) return s;
-  return dev_->InitComm(id, GetWorldSize(), rank_, MakeProbe());
+  bool same_host = true, dup_gpu = false, all_peers = true;
+  for (int r = 0; r < n; ++r) {
+    same_host = same_host && std::strncmp(all[r].host, all[0].host, sizeof(rec.host)) == 0;
+    all_peers = all_peers && all[r].stage_bytes != 0;
+    for (int q = 0; q < r; ++q) {
+      dup_gpu = dup_gpu || (std::strncmp(all[r].host, all[q].host, sizeof(rec.host)) == 0 &&
+                            std::strncmp(all[r].pci, all[q].pci, sizeof(rec.pci)) == 0);
+    }
+  }
+  // 2. direct transport: map the peers' buffers; every rank must succeed (min-allreduce)
+  int ok = 0;
+  if (have_peers && all_peers && same_host) {
+    ok = dev_->OpenPeers(all, rank_, &why) ? 1 : 0;
+    if (!ok) utils::HandleLogInfo("[%d] direct transport: %s\n", rank_, why.c_str());
+  }
+  s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  if (!ok) dev_->DropPeers();
+  // 3. RCCL: RCCL refuses several ranks on one GPU, which the direct transport handles alone
+  const bool want_rccl = dcfg_.algo != 2 && !dup_gpu;
+  if (want_rccl) {
+    std::string id(sizeof(ncclUniqueId), '\0');
+    if (rank_ == 0) id = device::DevicePlane::NewUniqueId();
+    s = host_->TreeBroadcast(&id[0], id.size(), 0);
+    if (s != Status::kSuccess) return s;
+    s = dev_->InitComm(id, n, rank_, MakeProbe());
+    if (s != Status::kSuccess) return s;
+  }
+  utils::Check(dev_->ready(),
+               "no device transport: ranks share a GPU (RCCL refuses) and the direct IPC "
+               "transport is %s",
+               dcfg_.algo == 1 ? "disabled (rabit_device_algo=rccl)" : "unavailable");
+  dev_->BeginEpoch(n, rank_);
+  if (dev_->has_comm() && dev_->has_peers() && dcfg_.algo == 0 && calibrate_) {
+    s = CalibrateDevice();
+    if (s != Status::kSuccess) return s;
+  }
+  if (debug_) {
+    utils::HandleLogInfo("[%d] device transport epoch %d: rccl=%d direct=%d (direct for >= %zu B)\n",
+                         rank_, dev_->epoch(), dev_->has_comm() ? 1 : 0,
+                         dev_->has_peers() ? 1 : 0, dcfg_.direct_min_bytes);
+  }
+  return Status::kSuccess;
 }
 
-Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec) {
+Status EngineBase::CalibrateDevice() {
+  // sizes in float32 elements; every rank runs the same sequence (this is a collective)
+  const size_t big = std::min<size_t>(32u << 20, dev_->has_peers() ? dcfg_.peer_stage : 0) / 4;
+  const size_t sizes[2] = {64u << 10, std::max<size_t>(big, 1u << 20)};
+  float *src = static_cast<float *>(dev_->Scratch(sizes[1] * 4, 0));
+  float *dst = static_cast<float *>(dev_->Scratch(sizes[1] * 4, 1));
+  const int n = GetWorldSize();
+  double t[2][2] = {{0, 0}, {0, 0}};  // [transport: 0 rccl, 1 direct][size]
+  int ok = 1;
+  dev_->SetPeerDeadline(5.0);
+  std::vector<float> host;
+  for (int which = 1; which >= 0; --which) {
+    for (int k = 0; k < 2 && ok; ++k) {
+      const size_t count = sizes[k];
+      device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, rank_ + 1.0, dev_->stream()),
+                       "LaunchFill");
+      dev_->ForceTransport(which);
+      double best = 1e30;
+      for (int rep = 0; rep < 4; ++rep) {
+        const double t0 = utils::GetTime();
+        Status st = dev_->Allreduce(src, dst, nullptr, count, mpi::kFloat, mpi::kSum,
+                                    device::kPrepCopy, 1.0, MakeProbe());
+        if (st == Status::kSuccess) st = dev_->Finish(MakeProbe());
+        if (st != Status::kSuccess) {
+          if (which == 0) {
+            dev_->ForceTransport(-1);
+            return st;  // RCCL failed: a real failure, let the caller recover
+          }
+          ok = 0;
+          break;
+        }
+        if (rep > 0) best = std::min(best, utils::GetTime() - t0);
+      }
+      if (!ok) break;
+      t[which][k] = best;
+      if (which == 1) {
+        // verify the direct result on the host: a broken peer mapping must not go unnoticed
+        host.resize(count);
+        dev_->StageToHost(host.data(), dst, count * 4);
+        const float want = 0.5f * n * (n + 1);
+        for (size_t i = 0; i < count && ok; ++i) ok = host[i] == want ? 1 : 0;
+        if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
+      }
+    }
+  }
+  dev_->ForceTransport(-1);
+  dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
+  // identical decision everywhere: max time over ranks, min of the verification flag
+  double agg[4] = {t[0][0], t[0][1], t[1][0], t[1][1]};
+  Status s = host_->Allreduce(agg, sizeof(double), 4, coll::HostReducer(mpi::kDouble, mpi::kMax));
+  if (s != Status::kSuccess) return s;
+  s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  size_t threshold = static_cast<size_t>(-1);
+  if (!ok) {
+    dev_->DropPeers();
+  } else {
+    // linear model t = a + b * bytes per transport through the two points; direct from the
+    // crossover on (when its slope is smaller)
+    const double x0 = sizes[0] * 4.0, x1 = sizes[1] * 4.0;
+    const double br = (agg[1] - agg[0]) / (x1 - x0), bd = (agg[3] - agg[2]) / (x1 - x0);
+    const double ar = agg[0] - br * x0, ad = agg[2] - bd * x0;
+    if (agg[3] < agg[1]) {
+      const double cross = bd < br ? (ad - ar) / (br - bd) : 0.0;
+      threshold = static_cast<size_t>(std::max(0.0, std::min(cross, x1)));
+    }
+    dev_->set_direct_min_bytes(threshold);
+  }
+  calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
+            static_cast<double>(sizes[1] * 4)};
+  if (debug_ || rank_ == 0) {
+    utils::HandleLogInfo(
+        "[xrabit] device calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B rccl "
+        "%.1f us direct %.1f us -> direct %s\n",
+        n, sizes[0] * 4, agg[0] * 1e6, agg[2] * 1e6, sizes[1] * 4, agg[1] * 1e6, agg[3] * 1e6,
+        !ok ? "disabled (failed verification)"
+            : (threshold == static_cast<size_t>(-1) ? "off (RCCL faster)"
+                                                    : ("from " + std::to_string(threshold) + " B").c_str()));
+  }
+  return Status::kSuccess;
+}
+
+Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec,
+                                      void *dst2, int prep, double alpha) {
   const size_t bytes = spec.bytes();
   if (bytes == 0) return Status::kSuccess;
+  if (dst2 == dst) dst2 = nullptr;
   bool rccl_ok = spec.builtin() && spec.dtype <= mpi::kULongLong;
   if (spec.builtin() && spec.op == mpi::kBitwiseOR &&
       (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble)) {
@@ -229,23 +389,32 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   dev_->EnterFromUser();
   if (!rccl_ok) {
     // user-defined reducer (host function): stage through host memory
+    utils::Check(prep == device::kPrepCopy, "fused prepare needs a built-in reduction");
     std::vector<uint64_t> tmp((bytes + 7) / 8);
     dev_->StageToHost(tmp.data(), src, bytes);
     Status s = TryAllreduceHost(tmp.data(), spec);
     if (s != Status::kSuccess) return s;
     dev_->StageToDevice(dst, tmp.data(), bytes);
+    if (dst2 != nullptr) dev_->CopyDeviceAsync(dst2, dst, bytes);
     return dev_->Finish(MakeProbe());
   }
   stats_.n_device_ops += 1;
   trace::Scope ts("device_allreduce", rank_, version_number_, seq_counter_, bytes, 1);
   if (GetWorldSize() == 1) {
     // a one-rank reduction is the identity: only materialise it where it was asked for
-    dev_->CopyDeviceAsync(dst, src, bytes);
+    if (prep != device::kPrepCopy) {
+      device::CheckHip(device::LaunchPrepare(dst, dst2, src, spec.count, spec.dtype, prep, alpha,
+                                             dev_->stream()),
+                       "LaunchPrepare");
+    } else {
+      dev_->CopyDeviceAsync(dst, src, bytes);
+      if (dst2 != nullptr && dst2 != src) dev_->CopyDeviceAsync(dst2, src, bytes);
+    }
     return dev_->Finish(MakeProbe());
   }
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
-  s = dev_->Allreduce(src, dst, spec.count, spec.dtype, spec.op, MakeProbe());
+  s = dev_->Allreduce(src, dst, dst2, spec.count, spec.dtype, spec.op, prep, alpha, MakeProbe());
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
 }
@@ -327,11 +496,11 @@ void EngineBase::DevAllreducePrepared(void *dst, const void *src, size_t count, 
                                       int op, int prep, double alpha, const char *, const int,
                                       const char *) {
   utils::Check(OnDevice(dst) && OnDevice(src), "DevAllreducePrepared needs device buffers");
-  dev_->EnterFromUser();
-  device::CheckHip(device::LaunchPrepare(dst, nullptr, src, count, dtype, prep, alpha,
-                                         dev_->stream()),
-                   "LaunchPrepare");
   if (GetWorldSize() == 1 && world1_fastpath_) {
+    dev_->EnterFromUser();
+    device::CheckHip(device::LaunchPrepare(dst, nullptr, src, count, dtype, prep, alpha,
+                                           dev_->stream()),
+                     "LaunchPrepare");
     utils::Check(dev_->Finish(MakeProbe()) == Status::kSuccess, "prepare failed");
     return;
   }
@@ -340,7 +509,8 @@ void EngineBase::DevAllreducePrepared(void *dst, const void *src, size_t count, 
   spec.count = count;
   spec.dtype = dtype;
   spec.op = op;
-  Status s = TryAllreduceDevice(dst, dst, spec);
+  // the prepare pass is fused into the transport (direct: it writes the stage buffer)
+  Status s = TryAllreduceDevice(src, dst, spec, nullptr, prep, alpha);
   utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));
   stats_.n_allreduce += 1;
 }
@@ -406,6 +576,12 @@ std::string EngineBase::StatsJson() const {
   os << "{\"engine\":\"" << EngineName() << "\",\"rank\":" << rank_
      << ",\"world_size\":" << GetWorldSize() << ",\"version\":" << version_number_
      << ",\"device\":" << GetDevice() << ",\"device_epoch\":" << (dev_ ? dev_->epoch() : 0)
+     << ",\"device_rccl\":" << (dev_ && dev_->has_comm() ? 1 : 0)
+     << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
+     << ",\"device_direct_min\":"
+     << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)
+     << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
+     << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
      << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
      << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
      << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops

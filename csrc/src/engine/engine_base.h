@@ -113,11 +113,20 @@ class EngineBase : public IEngine {
    * \brief device allreduce dst = reduce(src) (src may equal dst); custom host reducers are
    *        staged through host memory
    */
-  Status TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec);
+  /*!
+   * \brief dst = allreduce(prep(src)); also written to dst2 (if given) once the op succeeded
+   *        on this rank.  prep is a device::PrepOp (kPrepCopy: none).
+   */
+  Status TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec,
+                            void *dst2 = nullptr, int prep = 0, double alpha = 1.0);
   Status TryBroadcast(void *buf, size_t size, int root);
   Status TryAllgather(void *buf, size_t total, size_t begin, size_t end, size_t prev_size);
-  /*! \brief build the RCCL communicator if missing (collective) */
+  /*! \brief build the device transports if missing (collective): exchange GPU records, map
+   *  the peers' buffers for the direct transport, build the RCCL communicator */
   Status EnsureDeviceComm();
+  /*! \brief auto mode: time RCCL and the direct transport at two sizes, verify the direct
+   *  result, and set the size from which ops go direct (collective) */
+  Status CalibrateDevice();
   /*! \brief (re)connect peer links through the tracker */
   bool ReconnectLinks(const char *cmd);
   /*! \brief true if any peer link hung up (used while waiting on device ops) */
@@ -142,6 +151,11 @@ class EngineBase : public IEngine {
   bool timeout_enabled_{false};
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
+  bool calibrate_{true};
+  /*! \brief last calibration: rccl small/big, direct small/big (s), small/big bytes */
+  struct {
+    double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes;
+  } calib_{0, 0, 0, 0, 0, 0};
   bool trace_spans_{false};
   bool trace_roctx_{false};
   size_t trace_capacity_{1 << 16};

@@ -212,18 +212,18 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
   const bool dev = OnDevice(buf);
   const size_t bytes = spec.bytes();
   auto run_prepare = [&]() {
+    // a device prepare (prep_src) is fused into the transport below, not run here
+    if (prepare_fun != nullptr) prepare_fun(prepare_arg);
+  };
+  if (GetWorldSize() == 1 && world1_fastpath_) {
     if (prep_src != nullptr) {
       dev_->EnterFromUser();
       device::CheckHip(device::LaunchPrepare(buf, nullptr, prep_src, spec.count, spec.dtype,
                                              prep_op, prep_alpha, dev_->stream()),
                        "LaunchPrepare");
-    } else if (prepare_fun != nullptr) {
-      prepare_fun(prepare_arg);
+      dev_->Finish(MakeProbe(), false);
     }
-  };
-  if (GetWorldSize() == 1 && world1_fastpath_) {
     run_prepare();
-    if (prep_src != nullptr) dev_->Finish(MakeProbe(), false);
     return;
   }
   if (bytes == 0) {
@@ -250,21 +250,17 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
     }
     Status s;
     if (dev) {
-      // RCCL reduces straight into the log slot; the user buffer keeps the input for retries
-      s = TryAllreduceDevice(buf, temp, spec);
+      // the collective writes the log slot, and the user buffer only once it succeeded on this
+      // rank, so a retry still finds the input (prep_src: the prepare pass runs in the
+      // transport and is skipped entirely when the result is recovered)
+      s = TryAllreduceDevice(prep_src != nullptr ? prep_src : buf, temp, spec, buf,
+                             prep_src != nullptr ? prep_op : device::kPrepCopy, prep_alpha);
     } else {
       std::memcpy(temp, buf, bytes);
       s = TryAllreduceHost(temp, spec);
     }
     if (CheckAndRecover(s)) {
-      if (dev) {
-        // local copy: order the user stream after it, no host wait.  With one rank the
-        // user buffer already holds the result.
-        if (GetWorldSize() > 1) dev_->CopyDeviceAsync(buf, temp, bytes);
-        dev_->Finish(MakeProbe(), false);
-      } else {
-        std::memcpy(buf, temp, bytes);
-      }
+      if (!dev) std::memcpy(buf, temp, bytes);
       break;
     }
     recovered = RecoverExec(buf, bytes, 0, seq_counter_, cur_cache_seq_, "Allreduce");

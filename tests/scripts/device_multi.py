@@ -1,0 +1,117 @@
+"""Multi-rank HBM collectives through the direct (IPC peer-memory) transport.
+
+All ranks share GPU 0 of the test box (RCCL refuses that, the direct transport does not), so
+this drives the same code path as 8 ranks on 8 GPUs: stage -> flag barrier -> multi-source
+reduce of peer segments -> barrier -> gather.  A 1 MiB stage buffer forces chunking.
+Expected values are computed independently on the host with numpy."""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+import rabit_amd as rabit
+
+lib = os.environ.get("XR_LIB", "standard")
+rabit.init(sys.argv[1:], lib=lib, rabit_device=0, rabit_device_peer_buffer="1M",
+           rabit_device_peer_timeout_sec=20)
+rank, world = rabit.get_rank(), rabit.get_world_size()
+dev = torch.device("cuda", 0)
+
+TORCH = {
+    np.int8: torch.int8, np.uint8: torch.uint8, np.int32: torch.int32, np.int64: torch.int64,
+    np.float32: torch.float32, np.float64: torch.float64,
+}
+
+
+def values(r, n, dt, op):
+    i = np.arange(n, dtype=np.int64)
+    if op == rabit.BITOR:
+        v = (1 << (r % 7)) | (i % 3)
+    elif op == rabit.SUM:
+        v = (i % 5) + r
+    else:
+        v = ((i * 7 + r * 13) % 29) - (10 if np.dtype(dt).kind != "u" else 0)
+    return v.astype(dt)
+
+
+def expected(n, dt, op):
+    vs = [values(r, n, dt, op) for r in range(world)]
+    if op == rabit.SUM:
+        return np.sum(np.stack(vs).astype(np.float64), axis=0).astype(dt)
+    if op == rabit.MAX:
+        return np.max(np.stack(vs), axis=0)
+    if op == rabit.MIN:
+        return np.min(np.stack(vs), axis=0)
+    out = vs[0]
+    for v in vs[1:]:
+        out = out | v
+    return out
+
+
+checked = 0
+for dt in (np.int8, np.uint8, np.int32, np.int64, np.float32, np.float64):
+    ops = [rabit.MAX, rabit.MIN, rabit.SUM]
+    if np.dtype(dt).kind in "iu":
+        ops.append(rabit.BITOR)
+    for op in ops:
+        for n in (1, 7, 1000, 65536 + 3, (3 << 20) // np.dtype(dt).itemsize + 5):
+            t = torch.from_numpy(values(rank, n, dt, op)).to(dev)
+            rabit.allreduce(t, op)
+            got = t.cpu().numpy()
+            exp = expected(n, dt, op)
+            assert np.array_equal(got, exp), (dt, op, n, got[:8], exp[:8])
+            checked += 1
+
+# fused lazy-prepare: dst = sum over ranks of src^2
+n = (1 << 19) + 11
+src = torch.arange(n, device=dev, dtype=torch.float32).remainder_(17).add_(rank)
+dst = torch.empty_like(src)
+rabit.allreduce_prepared(dst, src, rabit.SUM, rabit.PREP_SQUARE)
+ref = sum((torch.arange(n, dtype=torch.float64).remainder(17) + r) ** 2 for r in range(world))
+assert torch.equal(dst.cpu().double(), ref), "prepared allreduce"
+
+# broadcast from every root, odd sizes and a chunked one
+for nbytes in (5, 4096 + 1, (1 << 20) * 2 + 3):
+    for root in range(world):
+        if rank == root:
+            b = torch.arange(nbytes, device=dev, dtype=torch.int64).remainder_(251).to(torch.uint8)
+        else:
+            b = torch.zeros(nbytes, device=dev, dtype=torch.uint8)
+        rabit.broadcast_tensor(b, root)
+        exp = torch.arange(nbytes, dtype=torch.int64).remainder(251).to(torch.uint8)
+        assert torch.equal(b.cpu(), exp), ("broadcast", nbytes, root)
+
+# allgather: equal slices through the Python API ...
+g = rabit.allgather(torch.full((1000,), float(rank), device=dev))
+assert torch.equal(g.cpu(), torch.arange(world).repeat_interleave(1000).float())
+# ... and rabit's variable slices through the C API (uint8, slice r has 100 + 37 r bytes)
+sizes = [100 + 37 * r for r in range(world)]
+begin = [sum(sizes[:r]) for r in range(world)]
+total = sum(sizes)
+buf = torch.zeros(total, device=dev, dtype=torch.uint8)
+buf[begin[rank]:begin[rank] + sizes[rank]] = rank + 1
+rabit.core._sync_stream_for(buf)
+rabit.lib().RabitAllgather(ctypes.c_void_p(buf.data_ptr()), total, begin[rank], sizes[rank],
+                           sizes[(rank - 1) % world], 1)
+exp = torch.cat([torch.full((sizes[r],), r + 1, dtype=torch.uint8) for r in range(world)])
+assert torch.equal(buf.cpu(), exp), "allgatherv"
+
+stats = rabit.stats()
+assert stats["device_direct"] == 1 and stats["device_rccl"] == 0, stats
+
+# a rough number for the log: 64 MiB fp32 sum, all ranks' traffic on the one shared GPU
+x = torch.ones(16 << 20, device=dev)
+rabit.allreduce(x, rabit.SUM)
+torch.cuda.synchronize()
+t0 = time.time()
+for _ in range(5):
+    rabit.allreduce(x, rabit.SUM)
+torch.cuda.synchronize()
+dt_ms = (time.time() - t0) / 5 * 1e3
+if rank == 0:
+    print("[%d] 64MiB direct allreduce on a shared GPU, world %d: %.2f ms" % (rank, world, dt_ms))
+rabit.finalize()
+print("[%d] DEVMULTI OK (%d allreduce cases)" % (rank, checked), flush=True)

@@ -1,0 +1,41 @@
+"""World > 1 HBM collectives on the GPU box: several ranks share its one GPU and talk through
+the direct IPC peer-memory transport (the path 8 ranks on 8 GPUs take over xGMI), including
+failure and replay of device results."""
+import os
+import sys
+
+import pytest
+
+from rabit_amd.launcher import LocalJob
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(script, nworker, args=(), attempts=1, timeout=300, env=None):
+    job = LocalJob([sys.executable, os.path.join(ROOT, "tests", "scripts", script)] + list(args),
+                   nworker, attempts, capture=True, timeout=timeout, print_fn=lambda m: None,
+                   env=env)
+    rc = job.run()
+    return rc, "".join("".join(o) for o in job.outputs)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_direct_collectives(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_multi.py", world)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVMULTI OK") == world, out[-3000:]
+
+
+@pytest.mark.parametrize("mock", [[], ["mock=1,1,0,0"], ["mock=0,2,1,0", "mock=2,1,2,0"]])
+def test_direct_recovery(mock):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_ft.py", 3, mock, attempts=4)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVFT OK") == 3, out[-3000:]
+    if mock:
+        assert "resumed at version" in out

@@ -25,6 +25,8 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python3 bench.py --steps 10 --warmup 3 ;;
+    multi) step multi 900 python -m pytest tests/test_gpu_multirank.py -x -q -p no:cacheprovider \
+             -k "${MULTI_K:-}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kbench) step kbench 300 python tools/kernel_bench.py ;;
     kprof) step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
