@@ -35,7 +35,7 @@ HEADERS   := $(shell find csrc -name '*.h')
 FLAVOURS  := rabit rabit_base rabit_mock rabit_empty
 LIBS      := $(foreach f,$(FLAVOURS),$(LIBDIR)/lib$(f).so) $(LIBDIR)/librabit_mock.a
 
-.PHONY: all libs tests clean
+.PHONY: all libs tests clean asan tsan
 all: libs
 libs: $(LIBS)
 
@@ -81,6 +81,15 @@ $(BIN)/%: tests/cpp/%.cc $(LIBDIR)/librabit_mock.so $(HEADERS)
 $(BIN)/%: examples/%.cc $(LIBDIR)/librabit.so $(HEADERS)
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lrabit -Wl,-rpath,$(abspath $(LIBDIR)) $(LDLIBS)
+
+# host sanitizer builds in their own tree (device code is not instrumented: GPU ASan / XNACK
+# are not available on the target pool).  tests/test_sanitizers.py runs the results.
+asan:
+	$(MAKE) BUILD=build/asan LIBDIR=build/asan/lib OPT=-O1 \
+	  SAN="-fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined" \
+	  libs tests
+tsan:
+	$(MAKE) BUILD=build/tsan LIBDIR=build/tsan/lib OPT=-O1 SAN="-fsanitize=thread" libs tests
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR)/*.so $(LIBDIR)/*.a

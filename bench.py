@@ -27,6 +27,73 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def _timed(rabit, torch, fn, reps, settle=0.0, device_wide=True):
+    """median wall time (s) of fn() over reps, ranks in lock step, max over ranks.
+    device_wide=False waits for the caller's stream only (work the library leaves running on
+    its own side streams, like a checkpoint's host mirror, is not on the caller's path)"""
+    times = []
+    for _ in range(reps):
+        if settle:
+            time.sleep(settle)  # e.g. let the previous checkpoint's host mirror finish
+        torch.cuda.synchronize()
+        rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+        t0 = time.perf_counter()
+        fn()
+        if device_wide:
+            torch.cuda.synchronize()
+        else:
+            torch.cuda.current_stream().synchronize()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return float(rabit.allreduce(np.array([med]), rabit.MAX)[0])
+
+
+def run_extras(rabit, torch, dev, world):
+    """BASELINE.json configs 3 and 4 plus the checkpoint cost of config 5, on this job's ranks
+    (result log and checkpoint paths included, as in the headline step)."""
+    out = {}
+    # config 3: Broadcast of a 1 GiB blob from root 0
+    nb = 1 << 30
+    blob = torch.empty(nb, dtype=torch.uint8, device=dev)
+    if rabit.get_rank() == 0:
+        blob.fill_(7)
+    rabit.broadcast_tensor(blob, 0)
+    ok = bool((blob[:: 1 << 20] == 7).all().item())
+    t = _timed(rabit, torch, lambda: rabit.broadcast_tensor(blob, 0), 3)
+    out["broadcast_1GiB_ms"] = round(t * 1e3, 3)
+    out["broadcast_1GiB_busbw_GBps"] = round(nb / t / 1e9, 2) if world > 1 else None
+    out["broadcast_check"] = ok
+    del blob
+    rabit.checkpoint(None)  # clears the result log (keeps HBM use bounded)
+    # config 4: lazy allreduce, prepare = per-element squared gradient, 64 MiB
+    n = (64 << 20) // 4
+    grad = torch.rand(n, dtype=torch.float32, device=dev)
+    acc = torch.empty_like(grad)
+
+    def fused():
+        rabit.allreduce_prepared(acc, grad, rabit.SUM, rabit.PREP_SQUARE)
+
+    def unfused():
+        torch.mul(grad, grad, out=acc)
+        rabit.allreduce(acc, rabit.SUM)
+
+    fused()
+    unfused()
+    out["lazy_sq_64MiB_fused_us"] = round(_timed(rabit, torch, fused, 5) * 1e6, 1)
+    out["lazy_sq_64MiB_unfused_us"] = round(_timed(rabit, torch, unfused, 5) * 1e6, 1)
+    rabit.checkpoint(None)
+    del grad, acc
+    # config 5 (checkpoint part): HBM snapshot of a 256 MiB model every iteration
+    model = torch.rand((256 << 20) // 4, dtype=torch.float32, device=dev)
+    rabit.checkpoint_tensors({"w": model}, meta={"it": 0})
+    # iterations longer than the async D2H mirror (~5 ms for 256 MiB) see only the snapshot
+    t = _timed(rabit, torch, lambda: rabit.checkpoint_tensors({"w": model}, meta={"it": 1}), 5,
+               settle=0.05, device_wide=False)
+    out["checkpoint_256MiB_us"] = round(t * 1e6, 1)
+    del model
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -35,6 +102,10 @@ def main():
     ap.add_argument("--size-mb", type=int, default=128)
     ap.add_argument("--engine", default="robust", choices=["robust", "base"])
     ap.add_argument("--check", type=int, default=1, help="verify one reduction first")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="after the timed loop, also time the other BASELINE configs: 1 GiB "
+                         "broadcast, 64 MiB lazy (squared-gradient) allreduce fused vs unfused, "
+                         "256 MiB HBM checkpoint")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -85,6 +156,8 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
 
+    extras = run_extras(rabit, torch, dev, world) if args.extras else {}
+
     t_step = elapsed / args.steps
     size_bytes = n * 4
     algbw = size_bytes / t_step / 1e9
@@ -115,6 +188,10 @@ def main():
         "baseline_note": "reference publishes no numbers (BASELINE.md)",
         "consensus_elided": st.get("n_consensus_elided", 0),
         "device_epoch": st.get("device_epoch", 0),
+        "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),
+                      "direct_min_bytes": st.get("device_direct_min", -1),
+                      "calibration_us": st.get("calib_us")},
+        "extras": extras,
     }
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -590,17 +590,20 @@ void EngineRobust::StopWatchdog() {
 void EngineRobust::WatchdogLoop() {
   std::unique_lock<std::mutex> lk(wd_mu_);
   while (!wd_stop_) {
-    wd_cv_.wait_for(lk, std::chrono::milliseconds(100));
+    // system_clock: wait_until then maps to pthread_cond_timedwait, which ThreadSanitizer
+    // understands (steady-clock waits use pthread_cond_clockwait, invisible to gcc-11 TSan)
+    wd_cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100));
     if (wd_stop_) break;
     const double since = recovering_since_.load();
     if (since > 0 && utils::GetTime() - since > timeout_sec_ && !watchdog_fired_.load()) {
       watchdog_fired_.store(true);
       // unblock whatever this rank is waiting on, then apply the timeout action
       abort_flag_.store(true);
+      const int rank = wd_rank_.load();
       if (timeout_handler_ != nullptr) {
-        timeout_handler_(rank_, timeout_sec_);
+        timeout_handler_(rank, timeout_sec_);
       } else {
-        fprintf(stderr, "[%d] xrabit: recovery did not finish within %d s, exiting\n", rank_,
+        fprintf(stderr, "[%d] xrabit: recovery did not finish within %d s, exiting\n", rank,
                 timeout_sec_);
         fflush(stderr);
         std::_Exit(253);

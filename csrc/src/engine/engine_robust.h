@@ -217,6 +217,7 @@ class EngineRobust : public EngineBase {
   bool wd_stop_{false};
   std::atomic<double> recovering_since_{0.0};
   std::atomic<bool> watchdog_fired_{false};
+  std::atomic<int> wd_rank_{-1};  // rank as seen by the watchdog thread (rank_ is not atomic)
 };
 }  // namespace engine
 }  // namespace rabit

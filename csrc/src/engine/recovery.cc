@@ -40,6 +40,7 @@ bool EngineRobust::CheckAndRecover(Status s) {
   fast_mode_ = false;
   recover_counter_ += 1;
   stats_.n_recover_events += 1;
+  wd_rank_.store(rank_);
   if (recovering_since_.load() == 0.0) recovering_since_.store(t0);
   if (debug_) {
     utils::HandleLogInfo("[%d] failure detected (%s, link %d), recovering\n", rank_,
@@ -53,6 +54,7 @@ bool EngineRobust::CheckAndRecover(Status s) {
   // spread the reconnect load on the tracker
   std::this_thread::sleep_for(std::chrono::milliseconds(10 * std::max(rank_, 0)));
   ReconnectLinks("recover");
+  wd_rank_.store(rank_);
   stats_.t_recover += utils::GetTime() - t0;
   return false;
 }
