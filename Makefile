@@ -24,7 +24,7 @@ CXXFLAGS  := $(OPT) -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pth
 HIPFLAGS  := $(OPT) -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(INC)
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
 
-CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc \
+CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc csrc/src/net/link_reset.cc \
              csrc/src/coll/host_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc csrc/src/device/peer_coll.cc \
              csrc/src/engine/engine_base.cc csrc/src/engine/engine_robust.cc \
              csrc/src/engine/recovery.cc csrc/src/capi/c_api.cc
@@ -69,12 +69,16 @@ $(LIBDIR)/librabit_mock.a: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_mock.o
 	rm -f $@ && ar rcs $@ $^
 
 # ---------------------------------------------------------------- test / example programs
-TEST_PROGS := unit_tests recover_test speed_test basic broadcast lazy_allreduce
+TEST_PROGS := unit_tests recover_test speed_test basic broadcast lazy_allreduce device_reducer_test
 tests: $(foreach p,$(TEST_PROGS),$(BIN)/$(p))
 
 $(BIN)/unit_tests: tests/cpp/unit_tests.cc $(LIBDIR)/librabit_mock.a $(HEADERS)
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) $< $(LIBDIR)/librabit_mock.a -o $@ $(LDLIBS)
+# a HIP program: the user's reduction is instantiated as a gfx950 kernel in its own TU
+$(BIN)/device_reducer_test: tests/cpp/device_reducer_test.hip $(LIBDIR)/librabit_mock.so $(HEADERS)
+	@mkdir -p $(BIN)
+	$(HIPCC) $(HIPFLAGS) $< -o $@ -L$(LIBDIR) -lrabit_mock -Wl,-rpath,$(abspath $(LIBDIR)) $(LDLIBS)
 $(BIN)/%: tests/cpp/%.cc $(LIBDIR)/librabit_mock.so $(HEADERS)
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lrabit_mock -Wl,-rpath,$(abspath $(LIBDIR)) $(LDLIBS)

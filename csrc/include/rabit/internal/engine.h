@@ -69,6 +69,15 @@ class IEngine {
   /*! \brief MPI-style reduce function; buffers are 8-byte aligned */
   typedef void(ReduceFunction)(const void *src, void *dst, int count, const MPI::Datatype &dtype);
 
+  /*!
+   * \brief launcher of a user-defined device reduction (rabit/device_reducer.h):
+   *        dst[i] = reduce(srcs[0][i], ..., srcs[nsrc-1][i]) for count elements, enqueued on the
+   *        HIP stream `stream`; when guard is non-null the kernel must do nothing if *guard != 0
+   *        at its start (a failed peer barrier).  dst may alias srcs[0].  Returns a hipError_t.
+   */
+  typedef int(DeviceReduceLauncher)(void *dst, const void *const *srcs, int nsrc, size_t count,
+                                    const int *guard, void *stream);
+
   virtual ~IEngine() = default;
   /*! \brief ring allgather: this rank owns [slice_begin, slice_end) of a ring buffer of
    *  total_size bytes; the slice of rank+1 starts at slice_end */
@@ -87,6 +96,16 @@ class IEngine {
                               PreprocFunction prepare_fun = nullptr, void *prepare_arg = nullptr,
                               const char *_file = _FILE, const int _line = _LINE,
                               const char *_caller = _CALLER);
+  /*!
+   * \brief in-place allreduce with a user reduction that has a device form: HBM buffers are
+   *        reduced by dev_reducer kernels on the device plane, host buffers by host_reducer.
+   *        Default implementation: host_reducer through Allreduce.
+   */
+  virtual void AllreduceDevice(void *sendrecvbuf_, size_t type_nbytes, size_t count,
+                               DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                               PreprocFunction prepare_fun = nullptr, void *prepare_arg = nullptr,
+                               const char *_file = _FILE, const int _line = _LINE,
+                               const char *_caller = _CALLER);
   /*! \brief broadcast size bytes from root */
   virtual void Broadcast(void *sendrecvbuf_, size_t size, int root, const char *_file = _FILE,
                          const int _line = _LINE, const char *_caller = _CALLER) = 0;

@@ -377,7 +377,11 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
     send = recv;
   }
   if (!RcclOp(op, &o)) {
-    Status s = AllreduceByKernel(send, recv, count, dtype, op, probe);
+    PeerGroup::ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
+                                             const int *guard, hipStream_t st) {
+      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard);
+    };
+    Status s = AllreduceByKernel(send, recv, count, TypeBytes(dtype), step, probe);
     if (s != Status::kSuccess) return s;
   } else {
     CheckNccl(ncclAllReduce(send, recv, count, t, o, comm_, stream_), "ncclAllReduce");
@@ -392,10 +396,34 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   return Status::kSuccess;
 }
 
-Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count, int dtype,
-                                      int op, const FailureProbe &probe) {
+Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
+                                    size_t type_nbytes, DeviceReduceLauncher *launcher,
+                                    const FailureProbe &probe) {
+  PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
+                                          const int *guard, hipStream_t st) {
+    return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
+  };
+  const size_t bytes = count * type_nbytes;
+  if (UseDirect(bytes)) {
+    CheckHip(peers_->AllreduceCustom(send, recv, recv2, count, type_nbytes, step),
+             "direct allreduce (custom)");
+    return Status::kSuccess;
+  }
+  Status s = AllreduceByKernel(send, recv, count, type_nbytes, step, probe);
+  if (s != Status::kSuccess) return s;
+  if (recv2 != nullptr && recv2 != recv) {
+    pending_dst_ = recv2;
+    pending_src_ = recv;
+    pending_bytes_ = bytes;
+  }
+  return Status::kSuccess;
+}
+
+Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count, size_t tn,
+                                      const PeerGroup::ReduceStep &step,
+                                      const FailureProbe &probe) {
   (void)probe;
-  const size_t tn = TypeBytes(dtype);
+  utils::Check(comm_ != nullptr, "device allreduce without communicator");
   const int n = nranks_;
   if (n == 1) {
     CopyDeviceAsync(recv, send, count * tn);
@@ -411,13 +439,13 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
   for (int k = 0; k < n; ++k) {
     const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
     if (hi > lo) {
-      CheckHip(hipMemcpyAsync(a + k * seg_bytes, static_cast<const char *>(send) + lo * tn,
-                              (hi - lo) * tn, hipMemcpyDeviceToDevice, stream_),
+      CheckHip(LaunchCopy(a + k * seg_bytes, static_cast<const char *>(send) + lo * tn,
+                          (hi - lo) * tn, stream_),
                "pack");
     }
   }
   CheckNccl(ncclAllToAll(a, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllToAll");
-  // reduce the n copies of my segment, 8 sources per kernel pass
+  // reduce the n copies of my segment, up to 8 sources per kernel pass
   char *mine = a + static_cast<size_t>(rank_) * seg_bytes;
   std::vector<const void *> srcs;
   int done = 0;
@@ -428,16 +456,15 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
       srcs.push_back(b + static_cast<size_t>(done) * seg_bytes);
       ++done;
     }
-    CheckHip(LaunchReduceMulti(mine, srcs.data(), static_cast<int>(srcs.size()), seg, dtype, op,
-                               stream_),
-             "LaunchReduceMulti");
+    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, stream_),
+             "allreduce reduce step");
   }
   CheckNccl(ncclAllGather(mine, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllGather");
   for (int k = 0; k < n; ++k) {
     const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
     if (hi > lo) {
-      CheckHip(hipMemcpyAsync(static_cast<char *>(recv) + lo * tn, b + k * seg_bytes,
-                              (hi - lo) * tn, hipMemcpyDeviceToDevice, stream_),
+      CheckHip(LaunchCopy(static_cast<char *>(recv) + lo * tn, b + k * seg_bytes,
+                          (hi - lo) * tn, stream_),
                "unpack");
     }
   }

@@ -140,6 +140,13 @@ class DevicePlane {
    */
   Status Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
                    int prep, double alpha, const FailureProbe &probe);
+  /*! \brief launcher of a user device reduction (IEngine::DeviceReduceLauncher) */
+  typedef int(DeviceReduceLauncher)(void *dst, const void *const *srcs, int nsrc, size_t count,
+                                    const int *guard, void *stream);
+  /*! \brief allreduce of count elements of type_nbytes with a user device reduction */
+  Status AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
+                         size_t type_nbytes, DeviceReduceLauncher *launcher,
+                         const FailureProbe &probe);
   Status Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe);
   /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place */
   Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
@@ -164,8 +171,8 @@ class DevicePlane {
 
  private:
   Status WaitEvent(hipEvent_t ev, const FailureProbe &probe);
-  Status AllreduceByKernel(const void *send, void *recv, size_t count, int dtype, int op,
-                           const FailureProbe &probe);
+  Status AllreduceByKernel(const void *send, void *recv, size_t count, size_t type_nbytes,
+                           const PeerGroup::ReduceStep &step, const FailureProbe &probe);
 
   DeviceConfig cfg_;
   int device_{-1};

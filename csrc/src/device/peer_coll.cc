@@ -166,10 +166,27 @@ hipError_t PeerGroup::Barrier() {
 
 hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_t count,
                                 int dtype, int op, int prep, double alpha) {
+  ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
+                                const int *guard, hipStream_t st) {
+    return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard);
+  };
+  return AllreduceImpl(send, recv, recv2, count, ElemBytes(dtype), dtype, prep, alpha, step);
+}
+
+hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
+                                      size_t type_nbytes, const ReduceStep &step) {
+  return AllreduceImpl(send, recv, recv2, count, type_nbytes, -1, kPrepCopy, 1.0, step);
+}
+
+hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, size_t count,
+                                    size_t tn, int dtype, int prep, double alpha,
+                                    const ReduceStep &step) {
   utils::Assert(opened_, "peer group not opened");
-  const size_t tn = ElemBytes(dtype);
-  const size_t quantum = 64 * static_cast<size_t>(n_);  // keeps segments 256-B aligned
+  // segments are multiples of 256 elements: 256-byte aligned for any element size
+  const size_t quantum = 256 * static_cast<size_t>(n_);
   const size_t chunk = std::max(quantum, (stage_bytes_ / tn) / quantum * quantum);
+  utils::Check(chunk * tn <= stage_bytes_, "peer stage buffer too small for %zu-byte elements",
+               tn);
   const char *in = static_cast<const char *>(send);
   char *out = static_cast<char *>(recv);
   char *out2 = static_cast<char *>(recv2);
@@ -184,14 +201,13 @@ hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_
       XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, in + off * tn, c, dtype, prep, alpha, stream_));
     }
     XRABIT_TRY_HIP(Barrier());
-    const size_t seg = RoundUp((c + n_ - 1) / n_, 64);
+    const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
     SegRange(c, seg, rank_, &lo, &hi);
     if (hi > lo) {
       const void *srcs[kMaxPeers];
       for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which) + lo * tn;  // rank order: identical
-      XRABIT_TRY_HIP(
-          LaunchReduceMulti(mine + lo * tn, srcs, n_, hi - lo, dtype, op, stream_, dev_status()));
+      XRABIT_TRY_HIP(step(mine + lo * tn, srcs, n_, hi - lo, dev_status(), stream_));
     }
     XRABIT_TRY_HIP(Barrier());
     CopyBatch b;

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstddef>
+#include <functional>
 #include <algorithm>
 #include <cstdint>
 #include <string>
@@ -97,6 +98,14 @@ class PeerGroup {
   // enqueue on the stream given at construction (the caller waits / checks status)
   hipError_t Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
                        int prep, double alpha);
+  /*! \brief reduction step of a custom allreduce: dst = reduce(srcs[0..n)) over count
+   *  elements on `stream`, doing nothing when *guard != 0 */
+  typedef std::function<hipError_t(void *dst, const void *const *srcs, int n, size_t count,
+                                   const int *guard, hipStream_t stream)>
+      ReduceStep;
+  /*! \brief allreduce of count elements of type_nbytes bytes with a caller-provided reduction */
+  hipError_t AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
+                             size_t type_nbytes, const ReduceStep &step);
   hipError_t Broadcast(void *buf, size_t bytes, int root);
   hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                         const std::vector<size_t> &size);
@@ -112,6 +121,8 @@ class PeerGroup {
 
  private:
   hipError_t Barrier();
+  hipError_t AllreduceImpl(const void *send, void *recv, void *recv2, size_t count, size_t tn,
+                           int dtype, int prep, double alpha, const ReduceStep &step);
   char *stage(int rank, int which) const;
   int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
   void NewBatch(CopyBatch *b) const {

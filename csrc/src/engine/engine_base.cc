@@ -387,6 +387,23 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     utils::Error("BitOR is not defined for floating point types");
   }
   dev_->EnterFromUser();
+  if (spec.dev_red != nullptr) {
+    // user-defined device reduction: same transports, the user's kernel reduces
+    utils::Check(prep == device::kPrepCopy, "fused prepare needs a built-in reduction");
+    stats_.n_device_ops += 1;
+    trace::Scope ts("device_allreduce", rank_, version_number_, seq_counter_, bytes, 1);
+    if (GetWorldSize() == 1) {
+      dev_->CopyDeviceAsync(dst, src, bytes);
+      if (dst2 != nullptr && dst2 != src) dev_->CopyDeviceAsync(dst2, src, bytes);
+      return dev_->Finish(MakeProbe());
+    }
+    Status s = EnsureDeviceComm();
+    if (s != Status::kSuccess) return s;
+    s = dev_->AllreduceCustom(src, dst, dst2, spec.count, spec.type_nbytes, spec.dev_red,
+                              MakeProbe());
+    if (s != Status::kSuccess) return s;
+    return dev_->Finish(MakeProbe());
+  }
   if (!rccl_ok) {
     // user-defined reducer (host function): stage through host memory
     utils::Check(prep == device::kPrepCopy, "fused prepare needs a built-in reduction");
@@ -484,6 +501,25 @@ void EngineBase::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, mp
   spec.host_red = reducer;
   spec.dtype = dtype;
   spec.op = op;
+  const double t0 = utils::GetTime();
+  Status s = OnDevice(buf) ? TryAllreduceDevice(buf, buf, spec) : TryAllreduceHost(buf, spec);
+  utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));
+  stats_.n_allreduce += 1;
+  stats_.bytes_allreduce += static_cast<double>(spec.bytes());
+  stats_.t_allreduce += utils::GetTime() - t0;
+}
+
+void EngineBase::AllreduceDevice(void *buf, size_t type_nbytes, size_t count,
+                                 DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                                 PreprocFunction prepare_fun, void *prepare_arg, const char *,
+                                 const int, const char *) {
+  if (prepare_fun != nullptr) prepare_fun(prepare_arg);
+  if (GetWorldSize() == 1 && world1_fastpath_) return;
+  ReduceSpec spec;
+  spec.type_nbytes = type_nbytes;
+  spec.count = count;
+  spec.host_red = host_reducer;
+  spec.dev_red = dev_reducer;
   const double t0 = utils::GetTime();
   Status s = OnDevice(buf) ? TryAllreduceDevice(buf, buf, spec) : TryAllreduceHost(buf, spec);
   utils::Check(s == Status::kSuccess, "Allreduce failed: %s", net::StatusName(s));

@@ -55,6 +55,10 @@ class EngineBase : public IEngine {
   void Allreduce(void *sendrecvbuf_, size_t type_nbytes, size_t count, ReduceFunction reducer,
                  PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
                  const int _line, const char *_caller) override;
+  void AllreduceDevice(void *sendrecvbuf_, size_t type_nbytes, size_t count,
+                       DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                       PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                       const int _line, const char *_caller) override;
   void AllreduceTyped(void *sendrecvbuf_, size_t count, mpi::DataType dtype, mpi::OpType op,
                       ReduceFunction reducer, PreprocFunction prepare_fun, void *prepare_arg,
                       const char *_file, const int _line, const char *_caller) override;
@@ -101,6 +105,7 @@ class EngineBase : public IEngine {
     size_t type_nbytes{1};
     size_t count{0};
     ReduceFn host_red{nullptr};
+    DeviceReduceLauncher *dev_red{nullptr};  // user device reduction (AllreduceDevice)
     int dtype{-1};
     int op{-1};
     size_t bytes() const { return type_nbytes * count; }

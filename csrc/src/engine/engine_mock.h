@@ -64,6 +64,16 @@ class EngineMock : public EngineRobust {
                                  _line, _caller);
     tsum_allreduce_ += utils::GetTime() - t0;
   }
+  void AllreduceDevice(void *buf, size_t type_nbytes, size_t count,
+                       DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                       PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                       const int _line, const char *_caller) override {
+    Verify("AllReduce");
+    const double t0 = utils::GetTime();
+    EngineRobust::AllreduceDevice(buf, type_nbytes, count, dev_reducer, host_reducer,
+                                  prepare_fun, prepare_arg, _file, _line, _caller);
+    tsum_allreduce_ += utils::GetTime() - t0;
+  }
   void DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype, int op,
                             int prep, double alpha, const char *_file, const int _line,
                             const char *_caller) override {

@@ -193,6 +193,18 @@ void EngineRobust::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, 
   AllreduceImpl(buf, spec, prepare_fun, prepare_arg, _file, _line, _caller);
 }
 
+void EngineRobust::AllreduceDevice(void *buf, size_t type_nbytes, size_t count,
+                                   DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                                   PreprocFunction prepare_fun, void *prepare_arg,
+                                   const char *_file, const int _line, const char *_caller) {
+  ReduceSpec spec;
+  spec.type_nbytes = type_nbytes;
+  spec.count = count;
+  spec.host_red = host_reducer;
+  spec.dev_red = dev_reducer;
+  AllreduceImpl(buf, spec, prepare_fun, prepare_arg, _file, _line, _caller);
+}
+
 void EngineRobust::DevAllreducePrepared(void *dst, const void *src, size_t count, int dtype,
                                         int op, int prep, double alpha, const char *_file,
                                         const int _line, const char *_caller) {

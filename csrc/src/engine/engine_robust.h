@@ -45,6 +45,10 @@ class EngineRobust : public EngineBase {
   void Allreduce(void *sendrecvbuf_, size_t type_nbytes, size_t count, ReduceFunction reducer,
                  PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
                  const int _line, const char *_caller) override;
+  void AllreduceDevice(void *sendrecvbuf_, size_t type_nbytes, size_t count,
+                       DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                       PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                       const int _line, const char *_caller) override;
   void AllreduceTyped(void *sendrecvbuf_, size_t count, mpi::DataType dtype, mpi::OpType op,
                       ReduceFunction reducer, PreprocFunction prepare_fun, void *prepare_arg,
                       const char *_file, const int _line, const char *_caller) override;

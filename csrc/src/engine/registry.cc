@@ -39,6 +39,15 @@ void IEngine::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, mpi::
                   _line, _caller);
 }
 
+void IEngine::AllreduceDevice(void *buf, size_t type_nbytes, size_t count,
+                              DeviceReduceLauncher *dev_reducer, ReduceFunction host_reducer,
+                              PreprocFunction prepare_fun, void *prepare_arg, const char *_file,
+                              const int _line, const char *_caller) {
+  (void)dev_reducer;
+  this->Allreduce(buf, type_nbytes, count, host_reducer, prepare_fun, prepare_arg, _file, _line,
+                  _caller);
+}
+
 namespace {
 struct ThreadEntry {
   std::unique_ptr<IEngine> engine;

@@ -10,6 +10,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/ioctl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -152,6 +153,16 @@ ssize_t TcpSocket::Send(const void *buf, size_t len) {
 }
 
 ssize_t TcpSocket::Recv(void *buf, size_t len) { return ::recv(fd_, buf, len, 0); }
+
+ssize_t TcpSocket::SendUrgent(char c) { return ::send(fd_, &c, 1, MSG_OOB | MSG_NOSIGNAL); }
+
+ssize_t TcpSocket::RecvUrgent(char *c) { return ::recv(fd_, c, 1, MSG_OOB); }
+
+int TcpSocket::AtMark() const {
+  int atmark = 0;
+  if (ioctl(fd_, SIOCATMARK, &atmark) < 0) return -1;
+  return atmark != 0 ? 1 : 0;
+}
 
 size_t TcpSocket::SendAll(const void *buf, size_t len) {
   const char *p = static_cast<const char *>(buf);

@@ -82,6 +82,12 @@ class TcpSocket {
   /*! \brief single non-blocking send/recv; -1 with errno on failure */
   ssize_t Send(const void *buf, size_t len);
   ssize_t Recv(void *buf, size_t len);
+  /*! \brief send one urgent (MSG_OOB) byte: marks a position in the byte stream */
+  ssize_t SendUrgent(char c);
+  /*! \brief read the pending urgent byte (clears POLLPRI); <0 if none */
+  ssize_t RecvUrgent(char *c);
+  /*! \brief 1 if the read position is at the urgent mark, 0 if not, -1 on error (SIOCATMARK) */
+  int AtMark() const;
   /*! \brief blocking loops; return bytes moved (short count means error / EOF) */
   size_t SendAll(const void *buf, size_t len);
   size_t RecvAll(void *buf, size_t len);

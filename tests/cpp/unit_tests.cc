@@ -21,6 +21,7 @@
 
 #include "coll/host_coll.h"
 #include "core/params.h"
+#include "net/link_reset.h"
 #include "engine/engine_mock.h"
 #include "engine/engine_robust.h"
 
@@ -335,6 +336,61 @@ void MaxPacked(Packed &dst, const Packed &src) {  // NOLINT(*)
   for (int i = 0; i < 3; ++i) dst.c[i] = std::max(dst.c[i], src.c[i]);
 }
 }  // namespace
+
+namespace {
+/*! \brief a connected loopback TCP pair */
+void LoopbackPair(rabit::net::TcpSocket *a, rabit::net::TcpSocket *b) {
+  rabit::net::TcpSocket lis;
+  lis.Create();
+  const int port = lis.BindRange(19500, 20500);
+  EXPECT(port > 0);
+  lis.Listen();
+  a->Create();
+  EXPECT(a->Connect("127.0.0.1", port));
+  *b = lis.Accept();
+}
+}  // namespace
+
+TEST(link_reset_discards_stale_bytes) {
+  // reference TryResetLinks (allreduce_robust.cc:567-679): stale bytes in both directions are
+  // dropped, the stream is usable afterwards
+  rabit::net::TcpSocket a, b;
+  LoopbackPair(&a, &b);
+  std::vector<char> junk_a(200000, 'x'), junk_b(50000, 'y');
+  EXPECT(a.SendAll(junk_a.data(), junk_a.size()) == junk_a.size());
+  EXPECT(b.SendAll(junk_b.data(), junk_b.size()) == junk_b.size());
+  std::vector<rabit::net::TcpSocket *> la = {&a}, lb = {&b};
+  rabit::net::Status ra = rabit::net::Status::kSockError, rb = ra;
+  std::thread t([&]() { rb = rabit::net::ResetLinks(lb, 5000); });
+  ra = rabit::net::ResetLinks(la, 5000);
+  t.join();
+  EXPECT(ra == rabit::net::Status::kSuccess && rb == rabit::net::Status::kSuccess);
+  a.SetNonBlock(false);
+  b.SetNonBlock(false);
+  EXPECT(a.SendAll("hello", 5) == 5);
+  char got[6] = {0};
+  EXPECT(b.RecvAll(got, 5) == 5 && std::string(got) == "hello");
+  EXPECT(b.SendAll("world", 5) == 5);
+  EXPECT(a.RecvAll(got, 5) == 5 && std::string(got) == "world");
+}
+
+TEST(link_reset_dead_peer_fails) {
+  rabit::net::TcpSocket a, b;
+  LoopbackPair(&a, &b);
+  b.Close();
+  std::vector<rabit::net::TcpSocket *> la = {&a};
+  const auto t0 = std::chrono::steady_clock::now();
+  EXPECT(rabit::net::ResetLinks(la, 3000) == rabit::net::Status::kSockError);
+  EXPECT(a.IsClosed());
+  EXPECT(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(3));
+}
+
+TEST(link_reset_silent_peer_times_out) {
+  rabit::net::TcpSocket a, b;
+  LoopbackPair(&a, &b);  // b never takes part
+  std::vector<rabit::net::TcpSocket *> la = {&a};
+  EXPECT(rabit::net::ResetLinks(la, 300) == rabit::net::Status::kSockError);
+}
 
 TEST(api_uninitialised_single_node) {
   EXPECT(rabit::GetWorldSize() == 1 && rabit::GetRank() == 0);
