@@ -159,7 +159,7 @@ DevicePlane::~DevicePlane() {
     ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kScratchSlots; ++i) {
     if (scratch_[i] != nullptr) (void)hipFree(scratch_[i]);
   }
   if (pinned_ != nullptr) (void)hipHostFree(pinned_);
@@ -229,6 +229,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
   DropPeers();
   try {
     peers_.reset(new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_));
+    if (cfg_.phase_timing) peers_->EnableTiming();
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();
@@ -247,6 +248,13 @@ bool DevicePlane::OpenPeers(const std::vector<PeerRecord> &all, int rank, std::s
     peers_.reset();
     return false;
   }
+  return true;
+}
+
+bool DevicePlane::DirectPhaseUs(double out[PeerGroup::kPhases], uint64_t *nops) const {
+  if (peers_ == nullptr || peers_->timed_ops() == 0) return false;
+  *nops = peers_->timed_ops();
+  for (int k = 0; k < PeerGroup::kPhases; ++k) out[k] = peers_->phase_ms()[k] * 1e3 / *nops;
   return true;
 }
 
@@ -278,6 +286,7 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
         }
         return Status::kAborted;
       }
+      if (peers_ != nullptr) peers_->CollectTiming();
       return Status::kSuccess;
     }
     if (e != hipErrorNotReady) CheckHip(e, "device collective");

@@ -47,6 +47,7 @@ struct DeviceConfig {
   size_t peer_stage{256u << 20};       // direct transport: bytes per stage buffer (x2 per rank)
   double peer_deadline_sec{120};       // direct transport: barrier gives up after this long
   size_t direct_min_bytes{1u << 20};   // auto: ops of at least this size use the direct path
+  bool phase_timing{false};            // direct transport: hipEvent timing of each phase
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -129,6 +130,8 @@ class DevicePlane {
   void SetPeerDeadline(double sec) {
     if (peers_ != nullptr) peers_->set_deadline_sec(sec);
   }
+  /*! \brief average per-phase time (us) of timed direct allreduces; false if none */
+  bool DirectPhaseUs(double out[PeerGroup::kPhases], uint64_t *nops) const;
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;
 
@@ -187,8 +190,9 @@ class DevicePlane {
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};
   size_t pending_bytes_{0};
-  void *scratch_[2]{nullptr, nullptr};
-  size_t scratch_bytes_[2]{0, 0};
+  static constexpr int kScratchSlots = 3;  // 0/1: all-to-all path, 2: host-buffer staging
+  void *scratch_[kScratchSlots]{nullptr, nullptr, nullptr};
+  size_t scratch_bytes_[kScratchSlots]{0, 0, 0};
   void *pinned_{nullptr};
   size_t pinned_bytes_{0};
 };

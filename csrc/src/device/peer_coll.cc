@@ -87,6 +87,9 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
 
 PeerGroup::~PeerGroup() {
   (void)hipSetDevice(device_);
+  if (timing_) {
+    for (auto &e : ev_) (void)hipEventDestroy(e);
+  }
   for (size_t r = 0; r < peer_base_.size(); ++r) {
     if (peer_base_[r] != nullptr && peer_base_[r] != base_) (void)hipIpcCloseMemHandle(peer_base_[r]);
   }
@@ -190,17 +193,23 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   const char *in = static_cast<const char *>(send);
   char *out = static_cast<char *>(recv);
   char *out2 = static_cast<char *>(recv2);
+  // per-phase timing of single-chunk ops (rabit_device_phase_timing=1)
+  const bool timed = timing_ && count <= chunk;
+  auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
     const int which = parity_;
     parity_ ^= 1;
     char *mine = stage(rank_, which);
+    XRABIT_TRY_HIP(mark(0));
     if (prep == kPrepCopy) {
       XRABIT_TRY_HIP(LaunchCopy(mine, in + off * tn, c * tn, stream_));
     } else {
       XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, in + off * tn, c, dtype, prep, alpha, stream_));
     }
+    XRABIT_TRY_HIP(mark(1));
     XRABIT_TRY_HIP(Barrier());
+    XRABIT_TRY_HIP(mark(2));
     const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
     SegRange(c, seg, rank_, &lo, &hi);
@@ -209,7 +218,9 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which) + lo * tn;  // rank order: identical
       XRABIT_TRY_HIP(step(mine + lo * tn, srcs, n_, hi - lo, dev_status(), stream_));
     }
+    XRABIT_TRY_HIP(mark(3));
     XRABIT_TRY_HIP(Barrier());
+    XRABIT_TRY_HIP(mark(4));
     CopyBatch b;
     NewBatch(&b);
     for (int p = 0; p < n_; ++p) {
@@ -219,8 +230,30 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
              (hi - lo) * tn);
     }
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    XRABIT_TRY_HIP(mark(5));
   }
+  timing_pending_ = timed;
   return hipSuccess;
+}
+
+void PeerGroup::EnableTiming() {
+  if (timing_) return;
+  for (auto &e : ev_) CheckHip(hipEventCreate(&e), "hipEventCreate(phase)");
+  timing_ = true;
+}
+
+void PeerGroup::CollectTiming() {
+  if (!timing_pending_) return;
+  timing_pending_ = false;
+  for (int k = 0; k < kPhases; ++k) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    phase_ms_[k] += ms;
+  }
+  ++timed_ops_;
 }
 
 hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root) {

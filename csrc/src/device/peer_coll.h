@@ -115,6 +115,13 @@ class PeerGroup {
   /*! \brief true when a barrier gave up (read after the stream drained) */
   bool failed() const;
   uint64_t barriers() const { return epoch_; }
+  /*! \brief record hipEvents between the phases of single-chunk allreduces */
+  void EnableTiming();
+  /*! \brief fold the last timed op into the phase totals (call after the stream drained) */
+  void CollectTiming();
+  static constexpr int kPhases = 5;  // stage copy, barrier, reduce, barrier, gather
+  const double *phase_ms() const { return phase_ms_; }
+  uint64_t timed_ops() const { return timed_ops_; }
   void set_deadline_sec(double sec) {
     deadline_ticks_ = static_cast<long long>(std::max(sec, 0.1) * clock_khz_ * 1000.0);
   }
@@ -143,6 +150,10 @@ class PeerGroup {
   int parity_{0};
   PeerRecord local_{};
   bool opened_{false};
+  bool timing_{false}, timing_pending_{false};
+  hipEvent_t ev_[kPhases + 1]{};
+  double phase_ms_[kPhases]{};
+  uint64_t timed_ops_{0};
 };
 
 }  // namespace device

@@ -86,6 +86,9 @@ void EngineBase::SetParam(const char *name, const char *val) {
     calibrate_ = false;  // an explicit threshold wins over the measured one
   }
   if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
+  if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
+  if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
+  if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
   if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
@@ -217,6 +220,23 @@ void EngineBase::ReportStatus() const {
 }
 
 Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
+  const size_t bytes = spec.bytes();
+  if (host_via_device_ && dev_ && GetWorldSize() > 1 && spec.builtin() && bytes >= host_dev_min_ &&
+      !(spec.op == mpi::kBitwiseOR && (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble))) {
+    // large host buffer on a GPU node: stage through HBM and use the device transports (the
+    // role of the reference's MPI engine: vendor collectives instead of TCP)
+    void *d = dev_->Scratch(bytes, 2);
+    Status s = EnsureDeviceComm();
+    if (s != Status::kSuccess) return s;
+    dev_->StageToDevice(d, buf, bytes);
+    stats_.n_device_ops += 1;
+    s = dev_->Allreduce(d, d, nullptr, spec.count, spec.dtype, spec.op, device::kPrepCopy, 1.0,
+                        MakeProbe());
+    if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+    if (s != Status::kSuccess) return s;
+    dev_->StageToHost(buf, d, bytes);
+    return Status::kSuccess;
+  }
   ReduceFn red = spec.host_red;
   if (spec.builtin()) {
     ReduceFn fast = coll::HostReducer(static_cast<mpi::DataType>(spec.dtype),
@@ -617,8 +637,15 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_direct_min\":"
      << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
-     << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
-     << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
+     << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]";
+  double phase[device::PeerGroup::kPhases];
+  uint64_t nphase = 0;
+  if (dev_ && dev_->DirectPhaseUs(phase, &nphase)) {
+    os << ",\"direct_timed_ops\":" << nphase << ",\"direct_phase_us\":{\"stage\":" << phase[0]
+       << ",\"barrier1\":" << phase[1] << ",\"reduce\":" << phase[2] << ",\"barrier2\":" << phase[3]
+       << ",\"gather\":" << phase[4] << "}";
+  }
+  os << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
      << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
      << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus

@@ -157,6 +157,8 @@ class EngineBase : public IEngine {
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
   bool calibrate_{true};
+  bool host_via_device_{false};     // stage large host-buffer allreduces through HBM
+  size_t host_dev_min_{1u << 20};
   /*! \brief last calibration: rccl small/big, direct small/big (s), small/big bytes */
   struct {
     double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes;

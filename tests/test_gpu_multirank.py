@@ -39,3 +39,11 @@ def test_direct_recovery(mock):
     assert out.count("DEVFT OK") == 3, out[-3000:]
     if mock:
         assert "resumed at version" in out
+
+
+def test_host_buffers_via_device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("host_via_device.py", 3)
+    assert rc == 0, out[-5000:]
+    assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
