@@ -4,15 +4,17 @@
  *
  * All kernels here are HBM-bandwidth bound (element-wise: no reuse), so the goal is the HBM
  * roof (~6.3-7 TB/s achievable on MI355X).  Structure, chosen by measurement
- * (tools/kernel_variants.hip, profiles/r1_s3_variants): a one-shot grid in which workgroup b
- * owns the contiguous tile of 256 x U 16-byte vectors starting at b*256*U:
+ * (tools/kernel_variants.hip; profiles/r1_s5_kernels, profiles/r1_s12_variants): a one-shot
+ * grid in which workgroup b owns the contiguous tile of 256 x U 16-byte vectors at b*256*U:
  *  - every wave instruction moves 1 KiB contiguous (64 lanes x 16 B: global_load_dwordx4);
- *  - all U (x sources) loads of a lane are issued before any arithmetic or store;
+ *  - U = 1 (32768 workgroups per 128 MiB): copy 39.7 us / dst += src 56.8 us, vs 41.2 / 58.6
+ *    at U = 4 and 44.4 / 66.8 for the best grid-stride loops (2048-4096 workgroups);
+ *  - all loads of a lane (x sources) are issued before any arithmetic or store;
  *  - the data is loaded as uint4 and re-interpreted in registers, so the compiler cannot split
  *    a 16-byte access into halves (it did with struct-of-T packs: 4.8 TB/s, half-width stores);
- *  - no grid-stride loop: 8192 workgroups for 128 MiB; the dispatcher balances them over the
- *    256 CUs / 8 XCDs (grid-stride at 2048 workgroups measured 5.0 TB/s for dst += src vs 6.9);
- *  - default cache policy: nontemporal loads/stores measured 6-9 % slower.
+ *  - stores to a buffer other than the one just read (multi-source reduce, prepare, dual
+ *    store) are nontemporal: two inputs -> third buffer 71 -> 57 us per 128 MiB; nontemporal
+ *    loads, and nontemporal stores for in-place / copy, measured neutral to 9 % slower.
  * MFMA is deliberately not used: an element-wise reduce has no data reuse; a ones-vector GEMM
  * over stacked peer buffers moves the same bytes and only adds matrix-pipe work.
  */
@@ -69,6 +71,14 @@ __device__ __forceinline__ uint4 Combine(uint4 a, uint4 b) {
 
 inline bool Aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+/*! \brief streaming (nontemporal) 16-byte store: for outputs that are not the buffer just read
+ *  (two inputs -> third buffer measured 71 -> 57 us per 128 MiB; neutral for in-place / copy) */
+__device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
+  u32x4_t w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
+}
+
 /*! \brief workgroups for a one-shot tile grid over nvec vectors (>= 1) */
 inline unsigned TileGrid(size_t nvec, int unroll) {
   size_t per = static_cast<size_t>(kBlock) * unroll;
@@ -123,7 +133,7 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
   T *d = static_cast<T *>(dst);
   const T *s = static_cast<const T *>(src);
   if (Aligned16(dst) && Aligned16(src)) {
-    constexpr int U = 4;
+    constexpr int U = 1;  // one 16-B vector per lane, 32768 workgroups per 128 MiB (fastest)
     hipLaunchKernelGGL((ReduceTileKernel<T, OP, U>), dim3(TileGrid(n * sizeof(T) / 16, U)),
                        dim3(kBlock), 0, st, d, s, n);
   } else {
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       uint4 acc = x[0][u];
 #pragma unroll
       for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, x[k][u]);
-      d[base + u * kBlock] = acc;
+      StoreNT(d + base + u * kBlock, acc);
     }
   } else {
     for (int u = 0; u < U; ++u) {
@@ -196,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcLis
 template <typename T, int OP, int NSRC>
 void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
   // keep ~8 16-byte loads in flight per lane
-  constexpr int U = NSRC >= 8 ? 1 : (NSRC >= 4 ? 2 : 4);
+  constexpr int U = 1;
   hipLaunchKernelGGL((ReduceMultiTileKernel<T, OP, NSRC, U>),
                      dim3(TileGrid(n * sizeof(T) / 16, U)), dim3(kBlock), 0, st, dst, sl, n);
 }
@@ -271,10 +281,10 @@ __global__ __launch_bounds__(kBlock) void PrepareTileKernel(T *dst, T *dst2, con
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = PrepVec<T>(a[u], prep, alpha);
 #pragma unroll
-    for (int u = 0; u < U; ++u) d[base + u * kBlock] = a[u];
+    for (int u = 0; u < U; ++u) StoreNT(d + base + u * kBlock, a[u]);
     if (d2 != nullptr) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) d2[base + u * kBlock] = a[u];
+      for (int u = 0; u < U; ++u) StoreNT(d2 + base + u * kBlock, a[u]);
     }
   } else {
     for (int u = 0; u < U; ++u) {
@@ -310,7 +320,7 @@ hipError_t Prepare(void *dst, void *dst2, const void *src, size_t n, int prep, d
   const T *s = static_cast<const T *>(src);
   const T a = static_cast<T>(alpha);
   if (Aligned16(dst) && Aligned16(src) && (dst2 == nullptr || Aligned16(dst2))) {
-    constexpr int U = 4;
+    constexpr int U = 1;
     hipLaunchKernelGGL((PrepareTileKernel<T, U>), dim3(TileGrid(n * sizeof(T) / 16, U)),
                        dim3(kBlock), 0, st, d, d2, s, n, prep, a);
   } else {
@@ -504,7 +514,7 @@ hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stre
   if (bytes == 0 || dst == src) return hipSuccess;
   const size_t nvec = Aligned16(dst) && Aligned16(src) ? bytes / 16 : 0;
   if (nvec != 0) {
-    constexpr int U = 4;
+    constexpr int U = 1;
     hipLaunchKernelGGL(CopyTileKernel<U>, dim3(TileGrid(nvec, U)), dim3(kBlock), 0, stream,
                        static_cast<uint4 *>(dst), static_cast<const uint4 *>(src), nvec);
     hipError_t e = hipGetLastError();

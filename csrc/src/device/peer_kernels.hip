@@ -29,7 +29,7 @@ namespace device {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 1;  // 4 KiB tiles: as for the streaming kernels of kernels.hip
 constexpr size_t kTileBytes = static_cast<size_t>(kBlock) * kUnroll * 16;
 
 __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int rank, int n,
@@ -58,6 +58,12 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
   __threadfence_system();
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
+  u32x4_t w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
+}
+
 __device__ __forceinline__ bool Al16(const void *p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
@@ -84,10 +90,10 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) v[u] = src[threadIdx.x + u * kBlock];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) dst[threadIdx.x + u * kBlock] = v[u];
+      for (int u = 0; u < kUnroll; ++u) StoreNT(dst + threadIdx.x + u * kBlock, v[u]);
       if (dst2 != nullptr) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) dst2[threadIdx.x + u * kBlock] = v[u];
+        for (int u = 0; u < kUnroll; ++u) StoreNT(dst2 + threadIdx.x + u * kBlock, v[u]);
       }
     } else {
       for (size_t i = threadIdx.x; i < nv; i += kBlock) {

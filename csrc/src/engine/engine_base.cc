@@ -86,6 +86,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
     calibrate_ = false;  // an explicit threshold wins over the measured one
   }
   if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
+  if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
@@ -650,6 +651,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
+     << ",\"n_device_replays\":" << s.n_device_replays
      << ",\"bytes_allreduce\":" << s.bytes_allreduce
      << ",\"bytes_broadcast\":" << s.bytes_broadcast
      << ",\"bytes_allgather\":" << s.bytes_allgather << ",\"t_allreduce\":" << s.t_allreduce

@@ -33,6 +33,7 @@ struct EngineStats {
   uint64_t n_allreduce{0}, n_broadcast{0}, n_allgather{0}, n_checkpoint{0};
   uint64_t n_device_ops{0}, n_recovered_ops{0}, n_recover_events{0}, n_consensus{0};
   uint64_t n_consensus_elided{0};
+  uint64_t n_device_replays{0};  // results recovered by a device broadcast (one xGMI hop)
   double bytes_allreduce{0}, bytes_broadcast{0}, bytes_allgather{0};
   double t_allreduce{0}, t_broadcast{0}, t_allgather{0}, t_checkpoint{0}, t_consensus{0};
   double t_recover{0};
@@ -157,6 +158,7 @@ class EngineBase : public IEngine {
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
   bool calibrate_{true};
+  bool device_replay_{true};       // recover HBM results with a device broadcast
   bool host_via_device_{false};     // stage large host-buffer allreduces through HBM
   size_t host_dev_min_{1u << 20};
   /*! \brief last calibration: rccl small/big, direct small/big (s), small/big bytes */

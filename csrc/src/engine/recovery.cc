@@ -11,7 +11,8 @@
  *    relaying through bounded staging rings on pass-through nodes;
  *  - local (per-rank) checkpoints are replicated to the next num_local_replica ring successors
  *    and recovered with one backward and one forward ring pass.
- * HBM-resident results are staged through host memory only on ranks that are on the route.
+ * HBM-resident results are broadcast on the device plane by one holder when every rank can
+ * take part (one xGMI hop), otherwise staged through host memory on the ranks of the route.
  */
 #include <algorithm>
 #include <chrono>
@@ -325,6 +326,28 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
                  "Allreduce recovered data size does not match the call (%zu vs %zu). Check "
                  "that the recovered program issues the same calls in this version",
                  data_size, size);
+  }
+  if (device_replay_) {
+    // one hop on the xGMI mesh: when every rank can take part on the device and a holder keeps
+    // the result in HBM, the lowest such holder broadcasts it (direct transport or RCCL)
+    // instead of streaming it through host memory along the TCP tree.  Every rank runs this
+    // agreement round (a rank without a device plane votes no).
+    int v[2];
+    v[0] = dev_ == nullptr ? 0 : (role == kPassData ? 1 : (data_dev ? 1 : 0));
+    v[1] = role == kHaveData && data_dev ? rank_ : std::numeric_limits<int>::max();
+    s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+    if (s != Status::kSuccess) return s;
+    if (v[0] == 1 && v[1] != std::numeric_limits<int>::max()) {
+      s = EnsureDeviceComm();
+      if (s != Status::kSuccess) return s;
+      const int root = v[1];
+      void *buf = role == kRequestData || rank_ == root ? data : dev_->Scratch(data_size, 2);
+      dev_->EnterFromUser();
+      s = dev_->Broadcast(buf, data_size, root, MakeProbe());
+      if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+      if (s == Status::kSuccess) stats_.n_device_replays += 1;
+      return s;
+    }
   }
   if (data_dev) {
     // HBM-resident: stage through host memory, only if this rank is on the route

@@ -108,10 +108,13 @@ class Poller {
   void WatchRead(int fd) { Entry(fd).events |= POLLIN; }
   void WatchWrite(int fd) { Entry(fd).events |= POLLOUT; }
   void WatchHangup(int fd) { Entry(fd).events |= POLLRDHUP; }
+  /*! \brief urgent (out-of-band) data, e.g. a link-reset mark (reference PollHelper::WatchException) */
+  void WatchExcept(int fd) { Entry(fd).events |= POLLPRI; }
   /*! \brief poll with a timeout in ms (-1 = infinite); returns poll()'s result */
   int Poll(int timeout_ms);
   bool CanRead(int fd) const { return Revents(fd) & (POLLIN | POLLHUP | POLLERR); }
   bool CanWrite(int fd) const { return Revents(fd) & (POLLOUT | POLLHUP | POLLERR); }
+  bool CanExcept(int fd) const { return Revents(fd) & POLLPRI; }
   bool HungUp(int fd) const { return Revents(fd) & (POLLRDHUP | POLLHUP | POLLERR | POLLNVAL); }
   bool Empty() const { return fds_.empty(); }
 

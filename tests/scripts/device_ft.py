@@ -39,4 +39,5 @@ assert torch.all(w == expect), (float(w[0]), expect)
 st = rabit.stats()
 assert st["device_direct"] == 1, st
 rabit.finalize()
-print("[%d] DEVFT OK" % rank, flush=True)
+print("[%d] DEVFT OK replays=%d recovered=%d" % (rank, st["n_device_replays"], st["n_recovered_ops"]),
+      flush=True)

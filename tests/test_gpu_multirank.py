@@ -39,6 +39,11 @@ def test_direct_recovery(mock):
     assert out.count("DEVFT OK") == 3, out[-3000:]
     if mock:
         assert "resumed at version" in out
+    if len(mock) == 2:
+        # the restarted ranks replayed logged HBM results: through the device broadcast path
+        import re
+        replays = [int(x) for x in re.findall(r"DEVFT OK replays=(\d+)", out)]
+        assert sum(replays) > 0, out[-3000:]
 
 
 def test_host_buffers_via_device():

@@ -97,11 +97,61 @@ __global__ __launch_bounds__(256) void KTile(uint4 *__restrict__ d, const uint4 
   }
 }
 
+// generalized tile: B lanes per block, U vectors per lane; XCD: tiles of one XCD contiguous
+// (workgroups are dispatched round-robin over the 8 XCDs); MODE 0 copy, 1 d += s, 2 o = d + s
+template <int B, int U, bool XCD, int MODE, bool NTS = false>
+__global__ __launch_bounds__(B) void KTileG(uint4 *__restrict__ d, const uint4 *__restrict__ s,
+                                            uint4 *__restrict__ o, size_t nvec) {
+  size_t tile = blockIdx.x;
+  if (XCD) {
+    const size_t g = gridDim.x, per = g / 8;
+    if (per * 8 == g) tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const size_t base = tile * B * U + threadIdx.x;
+  uint4 *out = MODE == 2 ? o : d;
+  if (base + (U - 1) * B < nvec) {
+    uint4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = s[base + u * B];
+    if (MODE != 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) b[u] = d[base + u * B];
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = add4(a[u], b[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NTS>(out + base + u * B, a[u]);
+  } else {
+    for (int u = 0; u < U; ++u) {
+      size_t i = base + u * B;
+      if (i < nvec) st<NTS>(out + i, MODE != 0 ? add4(s[i], d[i]) : s[i]);
+    }
+  }
+}
+
 struct Variant {
   std::string name;
   std::function<void(uint4 *, const uint4 *, size_t, hipStream_t)> run;
   bool add;
 };
+
+static uint4 *g_out = nullptr;  // third buffer for out-of-place variants
+static uint4 *g_out_base = nullptr;
+
+template <int B, int U, bool XCD, int MODE, bool NTS = false, int OFF = 0>
+Variant TileG() {
+  char nm[96];
+  const char *m = MODE == 0 ? "copy" : (MODE == 1 ? "add" : "add3");
+  snprintf(nm, sizeof(nm), "%s_tileg_b%d_u%d%s%s_off%d", m, B, U, XCD ? "_xcd" : "",
+           NTS ? "_nts" : "", OFF);
+  return {nm,
+          [](uint4 *d, const uint4 *s, size_t n, hipStream_t st) {
+            size_t g = (n + (size_t)B * U - 1) / ((size_t)B * U);
+            uint4 *o = g_out_base + OFF / 16;
+            hipLaunchKernelGGL((KTileG<B, U, XCD, MODE, NTS>), dim3(g), dim3(B), 0, st, d, s, o, n);
+          },
+          MODE != 0};
+}
 
 template <int U, bool NT, bool ADD>
 Variant Stride(int grid) {
@@ -132,6 +182,8 @@ int main(int argc, char **argv) {
   CHECK(hipMalloc(&a, bytes));
   CHECK(hipMalloc(&b, bytes));
   CHECK(hipMalloc(&c, bytes));
+  CHECK(hipMalloc(&g_out_base, bytes + (1 << 20)));
+  g_out = g_out_base;
   std::vector<float> h(bytes / 4);
   for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) * 1e-3f;
   CHECK(hipMemcpy(a, h.data(), bytes, hipMemcpyHostToDevice));
@@ -145,6 +197,20 @@ int main(int argc, char **argv) {
       Stride<8, false, true>(2048),  Stride<2, false, true>(4096),  Tile<4, false, true>(),
       Tile<8, false, true>(),        Tile<8, true, true>(),         Tile<2, false, true>(),
   };
+  {
+    std::vector<Variant> more = {
+        TileG<256, 4, false, 0>(),  TileG<256, 4, true, 0>(),   TileG<512, 4, false, 0>(),
+        TileG<1024, 2, false, 0>(), TileG<128, 1, false, 0>(),  TileG<256, 1, false, 0>(),
+        TileG<256, 2, true, 0>(),   TileG<256, 4, false, 1>(),  TileG<256, 4, true, 1>(),
+        TileG<512, 2, false, 1>(),  TileG<128, 1, false, 1>(),  TileG<256, 1, false, 1>(),
+        TileG<256, 4, false, 2>(),  TileG<256, 1, false, 2>(),  TileG<128, 1, false, 2>(),
+        TileG<256, 2, true, 2>(),
+        TileG<256, 1, false, 2, true>(),  TileG<256, 1, false, 0, true>(),
+        TileG<256, 1, false, 2, false, 4096>(), TileG<256, 1, false, 2, false, 65536>(),
+        TileG<256, 1, false, 2, false, 256>(),  TileG<256, 1, false, 1, true>(),
+    };
+    vs.insert(vs.end(), more.begin(), more.end());
+  }
   vs.push_back({"copy_hipMemcpyAsync",
                 [bytes](uint4 *d, const uint4 *s, size_t, hipStream_t st) {
                   (void)hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, st);
