@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/trace.h"
@@ -21,15 +22,59 @@ namespace rabit {
 namespace engine {
 
 // ------------------------------------------------------------------ ResultLog
+EngineRobust::ResultLog::HostArena::~HostArena() {
+  for (auto &c : chunks_) std::free(c.base);
+}
+
+void *EngineRobust::ResultLog::HostArena::Alloc(size_t bytes) {
+  const size_t need = (bytes + 63) & ~static_cast<size_t>(63);
+  while (cur_ < chunks_.size()) {
+    Chunk &c = chunks_[cur_];
+    if (c.size - c.used >= need) {
+      void *p = c.base + c.used;
+      c.used += need;
+      return p;
+    }
+    if (cur_ + 1 == chunks_.size()) break;
+    ++cur_;
+  }
+  Chunk c;
+  c.size = std::max<size_t>(need, 64u << 20);
+  c.base = static_cast<char *>(std::aligned_alloc(64, (c.size + 63) & ~static_cast<size_t>(63)));
+  utils::Check(c.base != nullptr, "out of host memory for the result log (%zu bytes)", c.size);
+  c.used = need;
+  chunks_.push_back(c);
+  cur_ = chunks_.size() - 1;
+  return c.base;
+}
+
+void EngineRobust::ResultLog::HostArena::PopTo(void *ptr) {
+  char *p = static_cast<char *>(ptr);
+  for (size_t i = 0; i < chunks_.size(); ++i) {
+    Chunk &c = chunks_[i];
+    if (p >= c.base && p < c.base + c.size) {
+      c.used = static_cast<size_t>(p - c.base);
+      for (size_t j = i + 1; j < chunks_.size(); ++j) chunks_[j].used = 0;
+      cur_ = i;
+      return;
+    }
+  }
+}
+
+void EngineRobust::ResultLog::HostArena::Reset() {
+  for (auto &c : chunks_) c.used = 0;
+  cur_ = 0;
+}
+
 void EngineRobust::ResultLog::Clear() {
   entries_.clear();
-  host_used_ = 0;
+  host_.Reset();
   if (arena_ != nullptr) arena_->Reset();
 }
 
 void *EngineRobust::ResultLog::AllocTemp(size_t size, bool device) {
   utils::Assert(size != 0, "cannot log a zero-size result");
-  temp_ = Entry{-1, size, device, 0, nullptr};
+  temp_ = Entry{-1, size, device, nullptr};
   if (device) {
     utils::Check(arena_ != nullptr, "device result without a device arena");
     void *p = arena_->Alloc(size);
@@ -37,13 +82,11 @@ void *EngineRobust::ResultLog::AllocTemp(size_t size, bool device) {
                  "device result log is full (%zu bytes logged since the last checkpoint); "
                  "checkpoint more often or raise rabit_device_log_cap",
                  arena_->used());
-    temp_.dev_ptr = p;
+    temp_.ptr = p;
     return p;
   }
-  const size_t words = (size + 7) / 8;
-  if (host_.size() < host_used_ + words) host_.resize(std::max(host_used_ + words, host_.size() * 2));
-  temp_.host_off = host_used_;
-  return host_.data() + host_used_;
+  temp_.ptr = host_.Alloc(size);
+  return temp_.ptr;
 }
 
 void EngineRobust::ResultLog::PushTemp(int seqno, size_t size) {
@@ -53,7 +96,6 @@ void EngineRobust::ResultLog::PushTemp(int seqno, size_t size) {
   }
   temp_.seqno = seqno;
   entries_.push_back(temp_);
-  if (!temp_.on_device) host_used_ += (size + 7) / 8;
 }
 
 const EngineRobust::ResultLog::Entry *EngineRobust::ResultLog::Query(int seqno) const {
@@ -68,9 +110,9 @@ void EngineRobust::ResultLog::DropLast() {
   const Entry e = entries_.back();
   entries_.pop_back();
   if (e.on_device) {
-    if (arena_ != nullptr) arena_->PopTo(e.dev_ptr);
+    if (arena_ != nullptr) arena_->PopTo(e.ptr);
   } else {
-    host_used_ = e.host_off;
+    host_.PopTo(e.ptr);
   }
 }
 

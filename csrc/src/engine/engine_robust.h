@@ -122,8 +122,7 @@ class EngineRobust : public EngineBase {
       int seqno;
       size_t size;
       bool on_device;
-      size_t host_off;  // in uint64 words
-      void *dev_ptr;
+      void *ptr;  // host arena or HBM arena slot
     };
     void SetArena(device::DeviceArena *a) { arena_ = a; }
     void Clear();
@@ -132,17 +131,32 @@ class EngineRobust : public EngineBase {
     void PushTemp(int seqno, size_t size);
     /*! \brief stored entry for seqno or nullptr */
     const Entry *Query(int seqno) const;
-    void *Data(const Entry &e) {
-      return e.on_device ? e.dev_ptr : static_cast<void *>(host_.data() + e.host_off);
-    }
+    void *Data(const Entry &e) { return e.ptr; }
     void DropLast();
     int LastSeqNo() const { return entries_.empty() ? -1 : entries_.back().seqno; }
     size_t size() const { return entries_.size(); }
 
    private:
+    /*! \brief host counterpart of device::DeviceArena: 64-byte aligned bump allocation over
+     *  chunks that are kept across checkpoints (no reallocation copies, no zero-fill, and
+     *  steady-state iterations touch no fresh pages) */
+    class HostArena {
+     public:
+      ~HostArena();
+      void *Alloc(size_t bytes);
+      void PopTo(void *ptr);
+      void Reset();
+
+     private:
+      struct Chunk {
+        char *base;
+        size_t size, used;
+      };
+      std::vector<Chunk> chunks_;
+      size_t cur_{0};
+    };
     std::vector<Entry> entries_;
-    std::vector<uint64_t> host_;
-    size_t host_used_{0};
+    HostArena host_;
     Entry temp_{};
     device::DeviceArena *arena_{nullptr};
   };
