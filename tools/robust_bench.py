@@ -1,0 +1,90 @@
+"""BASELINE config 5: fault-tolerant iterations — a 256 MiB Sum allreduce plus a CheckPoint every
+iteration, with one worker killed mid-run by the mock engine and recovered.
+
+    python -m rabit_amd.launcher -n 4 --num-attempt 2 python tools/robust_bench.py mock=3,4,0,0
+
+Each iteration of every rank: grad = model * 1e-3 + rank (HBM), allreduce(grad, SUM) on the
+device plane, model += grad, checkpoint_tensors({model}) (HBM snapshot + async pinned mirror).
+Without a GPU the same loop runs on numpy arrays over TCP (16 MiB).  The mock key
+`mock=r,v,s,t` kills rank r at its s-th collective after checkpoint v (trial t); the launcher
+restarts it, it reloads the model from a survivor's snapshot and replays what it missed.
+
+Every rank prints one JSON line: per-iteration wall times, time spent in checkpoints, and —
+for the restarted rank — the time from process start to being back in step.  Rank 0's line
+carries the summary (steady-state iteration median, the slowest iteration = the one that
+absorbed the failure).
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+T_START = time.time()
+import rabit_amd as rabit  # noqa: E402
+
+
+def main():
+    args = [a for a in sys.argv[1:] if "=" in a]
+    iters = int(os.environ.get("XR_ITERS", "10"))
+    try:
+        import torch
+        gpu = torch.cuda.is_available()
+    except ImportError:
+        gpu = False
+    rabit.init(args, lib="mock", **({"rabit_device": 0} if gpu else {}))
+    rank, world = rabit.get_rank(), rabit.get_world_size()
+    attempt = int(os.environ.get("DMLC_NUM_ATTEMPT", "0"))
+    nbytes = (256 << 20) if gpu else (16 << 20)
+    n = nbytes // 4
+    if gpu:
+        dev = torch.device("cuda", 0)
+        model = torch.zeros(n, device=dev)
+        version, meta = rabit.load_checkpoint_tensors({"model": model})
+    else:
+        version, state = rabit.load_checkpoint()
+        model = state if version else np.zeros(n, dtype=np.float32)
+    t_loaded = time.time()
+    iter_t, ckpt_t = [], []
+    for it in range(version, iters):
+        t0 = time.time()
+        if gpu:
+            grad = model * 1e-3 + rank
+            rabit.allreduce(grad, rabit.SUM)
+            model.add_(grad)
+            torch.cuda.current_stream().synchronize()
+        else:
+            grad = model * 1e-3 + rank
+            grad = rabit.allreduce(grad, rabit.SUM)
+            model += grad
+        t1 = time.time()
+        if gpu:
+            rabit.checkpoint_tensors({"model": model}, meta={"it": it + 1})
+            torch.cuda.current_stream().synchronize()
+        else:
+            rabit.checkpoint(model)
+        t2 = time.time()
+        iter_t.append(t2 - t0)
+        ckpt_t.append(t2 - t1)
+    # closed form check: every iteration adds world*(world-1)/2 + 1e-3*world*model
+    st = rabit.stats()
+    rec = {"rank": rank, "world": world, "attempt": attempt, "device": gpu,
+           "bytes": nbytes, "start_version": version,
+           "iter_ms": [round(t * 1e3, 2) for t in iter_t],
+           "checkpoint_ms": [round(t * 1e3, 3) for t in ckpt_t],
+           "recoveries": st["n_recover_events"], "recovered_ops": st["n_recovered_ops"],
+           "device_replays": st.get("n_device_replays", 0)}
+    if attempt > 0:
+        rec["restart_to_loaded_s"] = round(t_loaded - T_START, 3)
+    if rank == 0 and iter_t:
+        steady = sorted(iter_t)[: max(1, len(iter_t) - 2)]
+        rec["summary"] = {"steady_iter_ms_median": round(float(np.median(steady)) * 1e3, 2),
+                          "slowest_iter_ms": round(max(iter_t) * 1e3, 2),
+                          "checkpoint_ms_median": round(float(np.median(ckpt_t)) * 1e3, 3)}
+    print("ROBUST " + json.dumps(rec), flush=True)
+    rabit.finalize()
+
+
+if __name__ == "__main__":
+    main()
