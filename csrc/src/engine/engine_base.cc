@@ -416,7 +416,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     if (GetWorldSize() == 1) {
       dev_->CopyDeviceAsync(dst, src, bytes);
       if (dst2 != nullptr && dst2 != src) dev_->CopyDeviceAsync(dst2, src, bytes);
-      return dev_->Finish(MakeProbe());
+      return dev_->Finish(MakeProbe(), false);  // no peer can fail: stream-ordered, no host wait
     }
     Status s = EnsureDeviceComm();
     if (s != Status::kSuccess) return s;
@@ -448,7 +448,9 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
       dev_->CopyDeviceAsync(dst, src, bytes);
       if (dst2 != nullptr && dst2 != src) dev_->CopyDeviceAsync(dst2, src, bytes);
     }
-    return dev_->Finish(MakeProbe());
+    // one rank: nothing can fail remotely, so the op is stream-ordered like any HIP library
+    // call (the host does not wait; later work on the caller's stream sees the result)
+    return dev_->Finish(MakeProbe(), false);
   }
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
