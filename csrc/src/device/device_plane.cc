@@ -146,14 +146,18 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   }
   device_ = dev % ndev;
   CheckHip(hipSetDevice(device_), "hipSetDevice");
-  CheckHip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  CheckHip(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  CheckHip(hipEventCreateWithFlags(&ev_switch_, hipEventDisableTiming), "hipEventCreate");
+  stream_ = cfg_.ops_on_user_stream ? user_stream_ : own_stream_;
   CheckHip(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
   CheckHip(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
   arena_.Configure(cfg.arena_chunk, cfg.arena_cap);
 }
 
 DevicePlane::~DevicePlane() {
-  if (stream_ != nullptr) (void)hipStreamSynchronize(stream_);
+  // the caller's stream may be gone by now: drain the device instead of that stream
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
   peers_.reset();
   if (comm_ != nullptr) {
     ncclCommDestroy(comm_);
@@ -165,7 +169,8 @@ DevicePlane::~DevicePlane() {
   if (pinned_ != nullptr) (void)hipHostFree(pinned_);
   if (ev_in_ != nullptr) (void)hipEventDestroy(ev_in_);
   if (ev_done_ != nullptr) (void)hipEventDestroy(ev_done_);
-  if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
+  if (ev_switch_ != nullptr) (void)hipEventDestroy(ev_switch_);
+  if (own_stream_ != nullptr) (void)hipStreamDestroy(own_stream_);
 }
 
 bool DevicePlane::IsDevicePtr(const void *p) const {
@@ -263,6 +268,16 @@ void DevicePlane::DropPeers() {
     (void)hipStreamSynchronize(stream_);
     peers_.reset();
   }
+}
+
+void DevicePlane::SetUserStream(hipStream_t s) {
+  user_stream_ = s;
+  if (!cfg_.ops_on_user_stream || s == stream_) return;
+  // keep collectives in issue order across a change of stream
+  CheckHip(hipEventRecord(ev_switch_, stream_), "hipEventRecord(switch)");
+  CheckHip(hipStreamWaitEvent(s, ev_switch_, 0), "hipStreamWaitEvent(switch)");
+  stream_ = s;
+  if (peers_ != nullptr) peers_->set_stream(s);
 }
 
 void DevicePlane::EnterFromUser() {

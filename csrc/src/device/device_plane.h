@@ -48,6 +48,7 @@ struct DeviceConfig {
   double peer_deadline_sec{120};       // direct transport: barrier gives up after this long
   size_t direct_min_bytes{1u << 20};   // auto: ops of at least this size use the direct path
   bool phase_timing{false};            // direct transport: hipEvent timing of each phase
+  bool ops_on_user_stream{true};       // enqueue collectives on the caller's stream
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -86,7 +87,12 @@ class DevicePlane {
 
   int device() const { return device_; }
   bool IsDevicePtr(const void *p) const;
-  void SetUserStream(hipStream_t s) { user_stream_ = s; }
+  /*!
+   * \brief the caller's stream.  With ops_on_user_stream (default) collectives are enqueued on
+   *        it directly — no cross-stream events per op; a change of stream is ordered after the
+   *        previous one, so collectives stay in issue order on the GPU.
+   */
+  void SetUserStream(hipStream_t s);
   hipStream_t stream() const { return stream_; }
   DeviceArena *arena() { return &arena_; }
   const DeviceConfig &config() const { return cfg_; }
@@ -179,8 +185,10 @@ class DevicePlane {
 
   DeviceConfig cfg_;
   int device_{-1};
-  hipStream_t stream_{nullptr};
+  hipStream_t stream_{nullptr};       // stream collectives are enqueued on
+  hipStream_t own_stream_{nullptr};   // private non-blocking stream (ops_on_user_stream=false)
   hipStream_t user_stream_{nullptr};
+  hipEvent_t ev_switch_{nullptr};
   hipEvent_t ev_in_{nullptr}, ev_done_{nullptr};
   ncclComm_t comm_{nullptr};
   int nranks_{0}, rank_{0}, epoch_{0};

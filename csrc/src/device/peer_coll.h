@@ -93,6 +93,7 @@ class PeerGroup {
    */
   bool Open(const std::vector<PeerRecord> &all, int rank, std::string *why);
   int size() const { return n_; }
+  void set_stream(hipStream_t s) { stream_ = s; }
   size_t stage_bytes() const { return stage_bytes_; }
 
   // enqueue on the stream given at construction (the caller waits / checks status)

@@ -89,6 +89,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
+  if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
