@@ -109,7 +109,28 @@ Serializable *DeviceCheckpoint::Loader(int n, void *const *ptrs, const size_t *n
   loader_.ptrs.assign(ptrs, ptrs + n);
   loader_.nbytes.assign(nbytes, nbytes + n);
   loaded_meta_.clear();
+  loader_active_ = true;
+  payload_delivered_ = false;
   return &loader_;
+}
+
+void DeviceCheckpoint::SaveHeader(const Serializable *snapshot, Stream *fo) const {
+  const Half &h = *static_cast<const Half *>(snapshot);
+  uint64_t ml = h.meta.size();
+  fo->Write(&ml, sizeof(ml));
+  if (ml != 0) fo->Write(h.meta.data(), ml);
+  uint64_t n = h.sizes.size();
+  fo->Write(&n, sizeof(n));
+  for (size_t s : h.sizes) {
+    uint64_t v = s;
+    fo->Write(&v, sizeof(v));
+  }
+}
+
+void *DeviceCheckpoint::SnapshotBuffer(const Serializable *snapshot, size_t i) const {
+  const Half &h = *static_cast<const Half *>(snapshot);
+  utils::Check(i < h.dev.size(), "snapshot buffer %zu out of range", i);
+  return h.dev[i];
 }
 
 void DeviceCheckpoint::LoaderImpl::Load(Stream *fi) {
@@ -125,6 +146,16 @@ void DeviceCheckpoint::LoaderImpl::Load(Stream *fi) {
                static_cast<unsigned long long>(n), ptrs.size());
   std::vector<uint64_t> sizes(n);
   for (auto &s : sizes) utils::Check(fi->Read(&s, sizeof(s)) == sizeof(s), "device checkpoint: size");
+  owner->loader_active_ = false;
+  if (owner->payload_delivered_) {
+    // the engine already broadcast the payloads into ptrs on the device
+    owner->payload_delivered_ = false;
+    for (size_t i = 0; i < n; ++i) {
+      utils::Check(sizes[i] == nbytes[i], "device checkpoint buffer %zu: %llu bytes, %zu given", i,
+                   static_cast<unsigned long long>(sizes[i]), nbytes[i]);
+    }
+    return;
+  }
   std::vector<char> host;
   for (size_t i = 0; i < n; ++i) {
     utils::Check(sizes[i] == nbytes[i], "device checkpoint buffer %zu: %llu bytes stored, %zu given",

@@ -13,7 +13,8 @@
  *   3. registration with the robust engine as a *lazy* checkpoint: bytes are produced (from the
  *      pinned mirror, after its event) only if a recovering peer requests them.
  * Wire format of the global checkpoint: uint64 meta_len, meta, uint64 n, n x uint64 size,
- * then the n payloads.
+ * then the n payloads.  A recovering worker that loads into HBM gets the header over TCP and
+ * the payloads by device broadcasts from a survivor's snapshot (EngineRobust::TryLoadCheckPoint).
  */
 #ifndef XRABIT_DEVICE_DEVICE_CHECKPOINT_H_
 #define XRABIT_DEVICE_DEVICE_CHECKPOINT_H_
@@ -43,6 +44,20 @@ class DeviceCheckpoint {
   Serializable *Loader(int n, void *const *ptrs, const size_t *nbytes);
   /*! \brief metadata of the last Load */
   const std::string &loaded_meta() const { return loaded_meta_; }
+
+  // ---- device-side recovery (the robust engine broadcasts snapshot buffers over xGMI)
+  /*! \brief true if s is one of this checkpoint's snapshot halves */
+  bool IsSnapshot(const Serializable *s) const { return s == &half_[0] || s == &half_[1]; }
+  /*! \brief the header of a snapshot: meta_len, meta, n, sizes (the payload format minus data) */
+  void SaveHeader(const Serializable *snapshot, Stream *fo) const;
+  /*! \brief HBM buffer i of a snapshot */
+  void *SnapshotBuffer(const Serializable *snapshot, size_t i) const;
+  /*! \brief a Loader is waiting for data (set by Loader(), cleared by its Load) */
+  bool loader_active() const { return loader_active_; }
+  const std::vector<void *> &loader_targets() const { return loader_.ptrs; }
+  const std::vector<size_t> &loader_sizes() const { return loader_.nbytes; }
+  /*! \brief the payload already reached the loader's buffers: its Load reads the header only */
+  void MarkPayloadDelivered() { payload_delivered_ = true; }
   /*! \brief bytes of HBM reserved by the two snapshot halves */
   size_t reserved_bytes() const;
 
@@ -73,6 +88,8 @@ class DeviceCheckpoint {
   int cur_{1};
   LoaderImpl loader_;
   std::string loaded_meta_;
+  bool loader_active_{false};
+  bool payload_delivered_{false};
 };
 }  // namespace device
 }  // namespace rabit

@@ -655,6 +655,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
      << ",\"n_device_replays\":" << s.n_device_replays
+     << ",\"n_device_ckpt_loads\":" << s.n_device_ckpt_loads
      << ",\"bytes_allreduce\":" << s.bytes_allreduce
      << ",\"bytes_broadcast\":" << s.bytes_broadcast
      << ",\"bytes_allgather\":" << s.bytes_allgather << ",\"t_allreduce\":" << s.t_allreduce

@@ -33,7 +33,8 @@ struct EngineStats {
   uint64_t n_allreduce{0}, n_broadcast{0}, n_allgather{0}, n_checkpoint{0};
   uint64_t n_device_ops{0}, n_recovered_ops{0}, n_recover_events{0}, n_consensus{0};
   uint64_t n_consensus_elided{0};
-  uint64_t n_device_replays{0};  // results recovered by a device broadcast (one xGMI hop)
+  uint64_t n_device_replays{0};
+  uint64_t n_device_ckpt_loads{0};  // checkpoint loads served by device broadcasts  // results recovered by a device broadcast (one xGMI hop)
   double bytes_allreduce{0}, bytes_broadcast{0}, bytes_allgather{0};
   double t_allreduce{0}, t_broadcast{0}, t_allgather{0}, t_checkpoint{0}, t_consensus{0};
   double t_recover{0};

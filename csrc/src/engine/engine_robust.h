@@ -183,6 +183,8 @@ class EngineRobust : public EngineBase {
   /*! \brief true on success; on error repair links (tracker "recover") and return false */
   bool CheckAndRecover(Status s);
   Status TryLoadCheckPoint(bool requester);
+  /*! \brief checkpoint load over the device plane (see recovery.cc); kAborted: not applicable */
+  Status TryLoadDeviceCheckPoint(RecoverType role);
   Status TryGetResult(void *buf, size_t size, int seqno, bool requester);
   Status TryDecideRouting(RecoverType role, size_t *p_size, int *p_recvlink,
                           std::vector<bool> *p_req_in);

@@ -388,6 +388,10 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
     utils::Check(state == 1 || state == 2,
                  "LoadCheckPoint: too many nodes failed, cannot recover local state");
   }
+  if (device_replay_) {
+    s = TryLoadDeviceCheckPoint(role);
+    if (s != Status::kAborted) return s;  // kAborted here: not applicable, use the TCP route
+  }
   if (role == kHaveData && global_lazycheck_ != nullptr) {
     // materialise a lazy checkpoint now that a peer needs the bytes
     global_checkpoint_.clear();
@@ -404,6 +408,75 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
   if (role == kRequestData) global_checkpoint_.resize(size);
   if (size == 0) return Status::kSuccess;
   return TryRecoverData(role, BeginPtr(global_checkpoint_), size, recv_link, req_in);
+}
+
+Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
+  // A device checkpoint (HBM snapshot) on the holders and an HBM loader on the requester: the
+  // lowest holder broadcasts the header over the TCP tree and every buffer on the device plane
+  // (one xGMI hop) instead of serialising the model through host memory.  Every rank runs the
+  // agreement round; kAborted (with no side effect) means "take the TCP route".
+  const bool holder_dev = role == kHaveData && global_lazycheck_ != nullptr && dev_ckpt_ &&
+                          dev_ckpt_->IsSnapshot(global_lazycheck_);
+  const bool req_dev = role == kRequestData && dev_ckpt_ && dev_ckpt_->loader_active();
+  int v[2];
+  v[0] = dev_ != nullptr && (role == kRequestData ? req_dev : holder_dev) ? 1 : 0;
+  v[1] = holder_dev ? rank_ : std::numeric_limits<int>::max();
+  Status s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  if (v[0] != 1 || v[1] == std::numeric_limits<int>::max()) return Status::kAborted;
+  const int root = v[1];
+  std::string hdr;
+  if (rank_ == root) {
+    utils::MemoryBufferStream fs(&hdr);
+    fs.Write(&version_number_, sizeof(version_number_));
+    dev_ckpt_->SaveHeader(global_lazycheck_, &fs);
+  }
+  uint64_t len = hdr.size();
+  s = host_->TreeBroadcast(&len, sizeof(len), root);
+  if (s != Status::kSuccess) return s;
+  hdr.resize(len);
+  s = host_->TreeBroadcast(&hdr[0], len, root);
+  if (s != Status::kSuccess) return s;
+  // parse: int version, u64 meta_len, meta, u64 n, n x u64 size
+  utils::MemoryFixSizeBuffer fs(&hdr[0], hdr.size());
+  int version = 0;
+  uint64_t ml = 0, n = 0;
+  utils::Check(fs.Read(&version, sizeof(version)) == sizeof(version) &&
+                   fs.Read(&ml, sizeof(ml)) == sizeof(ml),
+               "device checkpoint header");
+  fs.Seek(sizeof(version) + sizeof(ml) + ml);
+  utils::Check(fs.Read(&n, sizeof(n)) == sizeof(n), "device checkpoint header count");
+  std::vector<uint64_t> sizes(n);
+  for (auto &z : sizes) utils::Check(fs.Read(&z, sizeof(z)) == sizeof(z), "header sizes");
+  if (role == kRequestData) {
+    utils::Check(dev_ckpt_->loader_targets().size() == n,
+                 "device checkpoint holds %llu buffers, %zu given",
+                 static_cast<unsigned long long>(n), dev_ckpt_->loader_targets().size());
+  }
+  s = EnsureDeviceComm();
+  if (s != Status::kSuccess) return s;
+  for (size_t i = 0; i < n; ++i) {
+    if (sizes[i] == 0) continue;
+    void *buf;
+    if (role == kRequestData) {
+      utils::Check(dev_ckpt_->loader_sizes()[i] == sizes[i],
+                   "device checkpoint buffer %zu: %llu bytes stored, %zu given", i,
+                   static_cast<unsigned long long>(sizes[i]), dev_ckpt_->loader_sizes()[i]);
+      buf = dev_ckpt_->loader_targets()[i];
+    } else {
+      buf = dev_ckpt_->SnapshotBuffer(global_lazycheck_, i);  // same bytes on every holder
+    }
+    dev_->EnterFromUser();
+    s = dev_->Broadcast(buf, sizes[i], root, MakeProbe());
+    if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+    if (s != Status::kSuccess) return s;
+  }
+  if (role == kRequestData) {
+    global_checkpoint_ = hdr;  // version + header; the payload is already in the targets
+    dev_ckpt_->MarkPayloadDelivered();
+  }
+  stats_.n_device_ckpt_loads += 1;
+  return Status::kSuccess;
 }
 
 Status EngineRobust::TryRestoreCache(bool requester, int min_seq, int max_seq) {

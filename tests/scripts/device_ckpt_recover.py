@@ -22,7 +22,8 @@ if version == 0:
 else:
     start = meta["next"]
     assert meta["tag"] == "xrabit", meta
-    print("[%d] reloaded version %d from peers" % (rank, version), flush=True)
+    print("[%d] reloaded version %d from peers (device loads %d)"
+          % (rank, version, rabit.stats()["n_device_ckpt_loads"]), flush=True)
 for it in range(start, 4):
     g = rabit.allreduce(np.full(4, float(rank + it)), rabit.SUM)  # host plane
     expect = sum(r + it for r in range(world))

@@ -1,5 +1,6 @@
-"""Fault tolerance with HBM state on the GPU box (several workers share its one GPU; their
-collectives use the host plane so no RCCL communicator spans a duplicated device)."""
+"""Fault tolerance with HBM state on the GPU box: several workers share its one GPU, collectives
+use host arrays, model checkpoints are HBM snapshots; a restarted worker's model comes back
+by device broadcasts (direct IPC transport) from a survivor's snapshot."""
 import os
 import sys
 
@@ -25,3 +26,7 @@ def test_device_checkpoint_recovery(mock):
     assert out.count("DEVCKPT OK") == 3
     if mock:
         assert "reloaded version" in out
+        # the model came back by device broadcasts from a survivor's HBM snapshot
+        import re
+        loads = [int(x) for x in re.findall(r"device loads (\d+)", out)]
+        assert loads and min(loads) >= 1, out[-3000:]
