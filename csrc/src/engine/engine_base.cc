@@ -86,6 +86,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
     calibrate_ = false;  // an explicit threshold wins over the measured one
   }
   if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
+  if (is("rabit_device_calibrate_test")) calibrate_test_ = utils::StringToBool(val);
   if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
@@ -304,7 +305,8 @@ Status EngineBase::EnsureDeviceComm() {
                "transport is %s",
                dcfg_.algo == 1 ? "disabled (rabit_device_algo=rccl)" : "unavailable");
   dev_->BeginEpoch(n, rank_);
-  if (dev_->has_comm() && dev_->has_peers() && dcfg_.algo == 0 && calibrate_) {
+  if ((dev_->has_comm() || calibrate_test_) && dev_->has_peers() && dcfg_.algo == 0 &&
+      calibrate_) {
     s = CalibrateDevice();
     if (s != Status::kSuccess) return s;
   }
@@ -327,47 +329,58 @@ Status EngineBase::CalibrateDevice() {
   int ok = 1;
   dev_->SetPeerDeadline(5.0);
   std::vector<float> host;
-  for (int which = 1; which >= 0; --which) {
-    for (int k = 0; k < 2 && ok; ++k) {
-      const size_t count = sizes[k];
-      device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, rank_ + 1.0, dev_->stream()),
-                       "LaunchFill");
-      dev_->ForceTransport(which);
-      double best = 1e30;
-      for (int rep = 0; rep < 4; ++rep) {
-        const double t0 = utils::GetTime();
-        Status st = dev_->Allreduce(src, dst, nullptr, count, mpi::kFloat, mpi::kSum,
-                                    device::kPrepCopy, 1.0, MakeProbe());
-        if (st == Status::kSuccess) st = dev_->Finish(MakeProbe());
-        if (st != Status::kSuccess) {
-          if (which == 0) {
-            dev_->ForceTransport(-1);
-            return st;  // RCCL failed: a real failure, let the caller recover
-          }
-          ok = 0;
-          break;
-        }
-        if (rep > 0) best = std::min(best, utils::GetTime() - t0);
-      }
-      if (!ok) break;
-      t[which][k] = best;
-      if (which == 1) {
-        // verify the direct result on the host: a broken peer mapping must not go unnoticed
-        host.resize(count);
-        dev_->StageToHost(host.data(), dst, count * 4);
-        const float want = 0.5f * n * (n + 1);
-        for (size_t i = 0; i < count && ok; ++i) ok = host[i] == want ? 1 : 0;
-        if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
-      }
+  // timed allreduce of sizes[k] on the forced transport; false on failure
+  auto measure = [&](int which, int k, Status *st) {
+    const size_t count = sizes[k];
+    device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, rank_ + 1.0, dev_->stream()),
+                     "LaunchFill");
+    // test hook: without RCCL (ranks sharing a GPU) the "RCCL" leg runs direct as well
+    dev_->ForceTransport(which == 0 && !dev_->has_comm() ? 1 : which);
+    double best = 1e30;
+    for (int rep = 0; rep < 4; ++rep) {
+      const double t0 = utils::GetTime();
+      *st = dev_->Allreduce(src, dst, nullptr, count, mpi::kFloat, mpi::kSum, device::kPrepCopy,
+                            1.0, MakeProbe());
+      if (*st == Status::kSuccess) *st = dev_->Finish(MakeProbe());
+      if (*st != Status::kSuccess) return false;
+      if (rep > 0) best = std::min(best, utils::GetTime() - t0);
     }
+    t[which][k] = best;
+    return true;
+  };
+  // 1. direct transport.  A rank stops at its first failure; its peers' next barrier then
+  //    times out (5 s deadline), so every rank leaves this phase in bounded time.
+  for (int k = 0; k < 2 && ok; ++k) {
+    Status st;
+    if (!measure(1, k, &st)) {
+      ok = 0;
+      break;
+    }
+    // verify the direct result on the host: a broken peer mapping must not go unnoticed
+    host.resize(sizes[k]);
+    dev_->StageToHost(host.data(), dst, sizes[k] * 4);
+    const float want = 0.5f * n * (n + 1);
+    for (size_t i = 0; i < sizes[k] && ok; ++i) ok = host[i] == want ? 1 : 0;
+    if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
   }
   dev_->ForceTransport(-1);
   dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
-  // identical decision everywhere: max time over ranks, min of the verification flag
-  double agg[4] = {t[0][0], t[0][1], t[1][0], t[1][1]};
-  Status s = host_->Allreduce(agg, sizeof(double), 4, coll::HostReducer(mpi::kDouble, mpi::kMax));
+  Status s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
-  s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  // 2. RCCL (only worth timing when the direct transport is usable: the choice is uniform)
+  if (ok) {
+    for (int k = 0; k < 2; ++k) {
+      Status st;
+      if (!measure(0, k, &st)) {
+        dev_->ForceTransport(-1);
+        return st;  // RCCL failed: a real failure, the caller recovers
+      }
+    }
+    dev_->ForceTransport(-1);
+  }
+  // identical decision everywhere: max time over ranks
+  double agg[4] = {t[0][0], t[0][1], t[1][0], t[1][1]};
+  s = host_->Allreduce(agg, sizeof(double), 4, coll::HostReducer(mpi::kDouble, mpi::kMax));
   if (s != Status::kSuccess) return s;
   size_t threshold = static_cast<size_t>(-1);
   if (!ok) {

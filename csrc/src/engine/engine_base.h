@@ -159,6 +159,7 @@ class EngineBase : public IEngine {
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
   bool calibrate_{true};
+  bool calibrate_test_{false};  // run the calibration without RCCL (tests on a shared GPU)
   bool device_replay_{true};       // recover HBM results with a device broadcast
   bool host_via_device_{false};     // stage large host-buffer allreduces through HBM
   size_t host_dev_min_{1u << 20};

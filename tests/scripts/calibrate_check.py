@@ -1,0 +1,26 @@
+"""Calibration control flow on a shared GPU (rabit_device_calibrate_test=1: the RCCL leg runs
+on the direct transport too).  Checks that every rank reports the same decision and that
+collectives of both sides of the threshold give correct results afterwards."""
+import sys
+
+import numpy as np
+import torch
+
+import rabit_amd as rabit
+
+rabit.init(sys.argv[1:], lib="standard", rabit_device=0, rabit_device_calibrate_test=1)
+rank, world = rabit.get_rank(), rabit.get_world_size()
+dev = torch.device("cuda", 0)
+for n in (1000, 3 << 20):
+    x = torch.full((n,), float(rank + 1), device=dev)
+    rabit.allreduce(x, rabit.SUM)
+    assert torch.all(x == world * (world + 1) / 2), n
+st = rabit.stats()
+calib = st["calib_us"]
+assert all(c > 0 for c in calib), calib
+thr = st["device_direct_min"]
+lo = rabit.allreduce(np.array([thr]), rabit.MIN)[0]
+hi = rabit.allreduce(np.array([thr]), rabit.MAX)[0]
+assert lo == hi, (lo, hi)
+rabit.finalize()
+print("[%d] CALIB OK thr=%s calib=%s" % (rank, thr, calib), flush=True)

@@ -52,3 +52,11 @@ def test_host_buffers_via_device():
     rc, out = _run("host_via_device.py", 3)
     assert rc == 0, out[-5000:]
     assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
+
+
+def test_calibration_flow():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("calibrate_check.py", 3)
+    assert rc == 0, out[-5000:]
+    assert out.count("CALIB OK") == 3, out[-3000:]
