@@ -76,6 +76,9 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
  *  (two inputs -> third buffer measured 71 -> 57 us per 128 MiB; neutral for in-place / copy) */
 __device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
   u32x4_t w = {v.x, v.y, v.z, v.w};
+  // compiler-only barrier: without it a later pass rebuilds this store as <4 x float> and drops
+  // the !nontemporal tag in the multi-source kernel (seen in the LLVM IR of hipcc, ROCm 7.2)
+  asm volatile("" ::: "memory");
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
 }
 
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       for (int k = 1; k < NSRC; ++k) {
         acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(srcs.p[k])[i]);
       }
-      d[i] = acc;
+      StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
     }
   }
   Tail<T>(nvec, n, [&](size_t i) {
@@ -291,8 +294,8 @@ __global__ __launch_bounds__(kBlock) void PrepareTileKernel(T *dst, T *dst2, con
       const size_t i = base + u * kBlock;
       if (i >= nvec) break;
       const uint4 y = PrepVec<T>(s[i], prep, alpha);
-      d[i] = y;
-      if (d2 != nullptr) d2[i] = y;
+      StoreNT(d + i, y);
+      if (d2 != nullptr) StoreNT(d2 + i, y);
     }
   }
   Tail<T>(nvec, n, [&](size_t i) {

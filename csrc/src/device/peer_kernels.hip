@@ -61,6 +61,9 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
   u32x4_t w = {v.x, v.y, v.z, v.w};
+  // compiler-only barrier: without it a later pass rebuilds this store as <4 x float> and drops
+  // the !nontemporal tag in the multi-source kernel (seen in the LLVM IR of hipcc, ROCm 7.2)
+  asm volatile("" ::: "memory");
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
 }
 
