@@ -102,6 +102,11 @@ def main():
     ap.add_argument("--size-mb", type=int, default=128)
     ap.add_argument("--engine", default="robust", choices=["robust", "base"])
     ap.add_argument("--check", type=int, default=1, help="verify one reduction first")
+    ap.add_argument("--symmetric", type=int, default=-1,
+                    help="allocate the buffer in rabit's symmetric heap (IPC-registered HBM that "
+                         "the direct transport reads in place, like registered buffers in "
+                         "nccl-tests); 0: a plain torch allocation (staged through a copy); "
+                         "-1 (default): symmetric when N > 1 (at N=1 nothing is exchanged)")
     ap.add_argument("--extras", type=int, default=1,
                     help="after the timed loop, also time the other BASELINE configs: 1 GiB "
                          "broadcast, 64 MiB lazy (squared-gradient) allreduce fused vs unfused, "
@@ -120,27 +125,33 @@ def main():
 
     torch.cuda.set_device(local_rank)
     # the rabit tracker lives in rank 0 next to the torchrun master port (rabit_amd.torchrun)
+    n = args.size_mb * (1 << 20) // 4
+    if args.symmetric < 0:
+        args.symmetric = 1 if world > 1 else 0
+    heap = {"rabit_device_symmetric_heap": str(n * 4 + (16 << 20))} if args.symmetric else {}
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
-                        rabit_world1_fastpath=0)
+                        rabit_world1_fastpath=0, **heap)
     dev = torch.device("cuda", local_rank)
 
     def barrier():
         rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
 
-    n = args.size_mb * (1 << 20) // 4
+    if args.symmetric:
+        x = rabit.symmetric_empty(n, torch.float32)
+    else:
+        x = torch.empty(n, dtype=torch.float32, device=dev)
     if args.check:
-        y = torch.full((n,), float(rabit.get_rank() + 1), dtype=torch.float32, device=dev)
-        rabit.allreduce(y, rabit.SUM)
+        x.fill_(float(rabit.get_rank() + 1))
+        rabit.allreduce(x, rabit.SUM)
         expect = world * (world + 1) / 2.0
-        ok = bool(torch.all(y == expect).item())
+        ok = bool(torch.all(x == expect).item())
         bad = rabit.allreduce(np.array([0 if ok else 1], dtype=np.int32), rabit.SUM)[0]
         if bad:
             raise SystemExit("allreduce result check failed on %d rank(s)" % bad)
-        del y
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     # |x| ~ 1e-3 keeps repeated in-place sums finite for hundreds of 8-rank steps
-    x = torch.rand((n,), generator=g, dtype=torch.float32, device=dev).mul_(1e-3)
+    x.copy_(torch.rand((n,), generator=g, dtype=torch.float32, device=dev).mul_(1e-3))
 
     for _ in range(args.warmup):
         rabit.allreduce(x, rabit.SUM)
@@ -179,7 +190,8 @@ def main():
         "data": "synthetic",
         "config": {"model": "rabit Allreduce<op::Sum> float32 x 32Mi (speed_test.cc shape)",
                    "global_batch": world, "seq_len": n, "parallelism": "dp%d" % world,
-                   "engine": args.engine, "size_bytes_per_rank": size_bytes},
+                   "engine": args.engine, "size_bytes_per_rank": size_bytes,
+                   "input_buffer": "symmetric heap" if args.symmetric else "torch allocation"},
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "t_us": round(t_step * 1e6, 1),
@@ -189,6 +201,7 @@ def main():
         "consensus_elided": st.get("n_consensus_elided", 0),
         "device_epoch": st.get("device_epoch", 0),
         "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),
+                      "zero_copy_chunks": st.get("zero_copy_chunks", 0),
                       "direct_min_bytes": st.get("device_direct_min", -1),
                       "calibration_us": st.get("calib_us")},
         "extras": extras,

@@ -81,6 +81,13 @@ RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes
  *         and the metadata blob (valid until the next call from this thread) */
 RABIT_DLL int RabitDevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                      char **out_meta, rbt_ulong *out_meta_len);
+/*!
+ * \brief allocate nbytes from the engine's symmetric heap (rabit_device_symmetric_heap=<size>):
+ *        HBM that the peers map through IPC, so an allreduce input placed there is read in
+ *        place by the direct transport (no stage copy).  NULL when unavailable or full; the
+ *        memory lives until RabitFinalize.
+ */
+RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

@@ -223,6 +223,12 @@ RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t coun
   });
 }
 
+RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) return nullptr;
+  return e->device_plane()->SymAlloc(nbytes);
+}
+
 RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                   const char *meta, rbt_ulong meta_len) {
   GuardVoid([&]() {

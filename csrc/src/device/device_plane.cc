@@ -152,6 +152,25 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   CheckHip(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
   CheckHip(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
   arena_.Configure(cfg.arena_chunk, cfg.arena_cap);
+  if (cfg.sym_heap > 0) {
+    // symmetric heap: uncached like the stage buffers (peers read it over xGMI in place)
+    heap_.bytes = (cfg.sym_heap + (1u << 16) - 1) & ~static_cast<size_t>((1u << 16) - 1);
+    void *p = nullptr;
+    CheckHip(hipExtMallocWithFlags(&p, heap_.bytes, hipDeviceMallocUncached),
+             "hipExtMallocWithFlags(symmetric heap)");
+    heap_.base = static_cast<char *>(p);
+    hipIpcMemHandle_t h;
+    CheckHip(hipIpcGetMemHandle(&h, heap_.base), "hipIpcGetMemHandle(heap)");
+    std::memcpy(heap_.ipc, &h, sizeof(h));
+  }
+}
+
+void *DevicePlane::SymAlloc(size_t bytes) {
+  const size_t need = (bytes + 255) & ~static_cast<size_t>(255);
+  if (heap_.base == nullptr || heap_used_ + need > heap_.bytes) return nullptr;
+  void *p = heap_.base + heap_used_;
+  heap_used_ += need;
+  return p;
 }
 
 DevicePlane::~DevicePlane() {
@@ -169,6 +188,8 @@ DevicePlane::~DevicePlane() {
   if (pinned_ != nullptr) (void)hipHostFree(pinned_);
   if (ev_in_ != nullptr) (void)hipEventDestroy(ev_in_);
   if (ev_done_ != nullptr) (void)hipEventDestroy(ev_done_);
+  peers_.reset();
+  if (heap_.base != nullptr) (void)hipFree(heap_.base);
   if (ev_switch_ != nullptr) (void)hipEventDestroy(ev_switch_);
   if (own_stream_ != nullptr) (void)hipStreamDestroy(own_stream_);
 }
@@ -233,7 +254,8 @@ void DevicePlane::DescribeDevice(PeerRecord *rec) const {
 bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
   DropPeers();
   try {
-    peers_.reset(new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_));
+    peers_.reset(
+        new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_, heap_));
     if (cfg_.phase_timing) peers_->EnableTiming();
   } catch (const std::exception &e) {
     peers_.reset();
@@ -402,8 +424,9 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   }
   if (!RcclOp(op, &o)) {
     PeerGroup::ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
-                                             const int *guard, hipStream_t st) {
-      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard);
+                                             const int *guard, const void *const *table,
+                                             hipStream_t st) {
+      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table);
     };
     Status s = AllreduceByKernel(send, recv, count, TypeBytes(dtype), step, probe);
     if (s != Status::kSuccess) return s;
@@ -424,7 +447,8 @@ Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, s
                                     size_t type_nbytes, DeviceReduceLauncher *launcher,
                                     const FailureProbe &probe) {
   PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
-                                          const int *guard, hipStream_t st) {
+                                          const int *guard, const void *const *,
+                                          hipStream_t st) {
     return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
   };
   const size_t bytes = count * type_nbytes;
@@ -480,7 +504,8 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
       srcs.push_back(b + static_cast<size_t>(done) * seg_bytes);
       ++done;
     }
-    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, stream_),
+    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, nullptr,
+                  stream_),
              "allreduce reduce step");
   }
   CheckNccl(ncclAllGather(mine, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllGather");

@@ -49,6 +49,7 @@ struct DeviceConfig {
   size_t direct_min_bytes{1u << 20};   // auto: ops of at least this size use the direct path
   bool phase_timing{false};            // direct transport: hipEvent timing of each phase
   bool ops_on_user_stream{true};       // enqueue collectives on the caller's stream
+  size_t sym_heap{0};                  // bytes of the symmetric (IPC-exported) heap, 0: none
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -138,6 +139,16 @@ class DevicePlane {
   }
   /*! \brief average per-phase time (us) of timed direct allreduces; false if none */
   bool DirectPhaseUs(double out[PeerGroup::kPhases], uint64_t *nops) const;
+  /*!
+   * \brief allocate from the symmetric heap: HBM that peers map through IPC, so the direct
+   *        transport reads an allreduce input there in place (no stage copy).  nullptr when
+   *        the heap is disabled (rabit_device_symmetric_heap=0) or full.  Bump allocation,
+   *        freed with the engine.
+   */
+  void *SymAlloc(size_t bytes);
+  const SymHeapInfo &sym_heap() const { return heap_; }
+  size_t sym_heap_used() const { return heap_used_; }
+  uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;
 
@@ -194,6 +205,8 @@ class DevicePlane {
   int nranks_{0}, rank_{0}, epoch_{0};
   DeviceArena arena_;
   std::unique_ptr<PeerGroup> peers_;
+  SymHeapInfo heap_;
+  size_t heap_used_{0};
   int force_{-1};
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};

@@ -29,10 +29,13 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 /*!
  * \brief dst[i] = op(srcs[0][i], ..., srcs[nsrc-1][i]), 1 <= nsrc <= 8 (dst may alias any
  *        source).  guard: optional device word; the launch does nothing when it is non-zero
- *        (set by a failed peer barrier earlier on the stream).
+ *        (set by a failed peer barrier earlier on the stream).  table: optional device array of
+ *        nsrc source pointers written by an earlier kernel (srcs then only serve the host-side
+ *        alignment check and must be aligned like the table's pointers).
  */
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
-                             int dtype, int op, hipStream_t stream, const int *guard = nullptr);
+                             int dtype, int op, hipStream_t stream, const int *guard = nullptr,
+                             const void *const *table = nullptr);
 /*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);

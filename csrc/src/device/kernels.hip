@@ -150,7 +150,14 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
 struct SrcList {
   const void *p[kMaxReduceSources];
   const int *guard;  // optional: skip the whole launch when *guard != 0 (failed peer barrier)
+  const void *const *table;  // optional: device table of source pointers (overrides p)
 };
+
+/*! \brief source k: from the device table when given (written by an earlier kernel, e.g. a
+ *  peer barrier that resolved where each peer's input lives), else the launch argument */
+__device__ __forceinline__ const void *Src(const SrcList &s, int k) {
+  return s.table != nullptr ? s.table[k] : s.p[k];
+}
 
 __device__ __forceinline__ bool Guarded(const int *guard) {
   return guard != nullptr &&
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[k][u] = reinterpret_cast<const uint4 *>(srcs.p[k])[base + u * kBlock];
+      for (int u = 0; u < U; ++u) x[k][u] = reinterpret_cast<const uint4 *>(Src(srcs, k))[base + u * kBlock];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -181,17 +188,17 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     for (int u = 0; u < U; ++u) {
       const size_t i = base + u * kBlock;
       if (i >= nvec) break;
-      uint4 acc = reinterpret_cast<const uint4 *>(srcs.p[0])[i];
+      uint4 acc = reinterpret_cast<const uint4 *>(Src(srcs, 0))[i];
       for (int k = 1; k < NSRC; ++k) {
-        acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(srcs.p[k])[i]);
+        acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(Src(srcs, k))[i]);
       }
       StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
     }
   }
   Tail<T>(nvec, n, [&](size_t i) {
-    T acc = static_cast<const T *>(srcs.p[0])[i];
+    T acc = static_cast<const T *>(Src(srcs, 0))[i];
 #pragma unroll
-    for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
+    for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
     dst[i] = acc;
   });
 }
@@ -201,8 +208,8 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcLis
                                                                   size_t n) {
   const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n || Guarded(srcs.guard)) return;
-  T acc = static_cast<const T *>(srcs.p[0])[i];
-  for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(srcs.p[k])[i]);
+  T acc = static_cast<const T *>(Src(srcs, 0))[i];
+  for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
   dst[i] = acc;
 }
 
@@ -216,9 +223,10 @@ void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
 
 template <typename T, int OP>
 hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st,
-                       const int *guard) {
+                       const int *guard, const void *const *table) {
   SrcList sl;
   sl.guard = guard;
+  sl.table = table;
   bool aligned = Aligned16(dst);
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;
@@ -466,8 +474,10 @@ struct OrTag {
     return hipErrorInvalidValue;
   }
   static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st,
-                            const int *guard) {
-    if constexpr (std::is_integral<T>::value) return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard);
+                            const int *guard, const void *const *table) {
+    if constexpr (std::is_integral<T>::value) {
+      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table);
+    }
     return hipErrorInvalidValue;
   }
 };
@@ -489,16 +499,17 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 }
 
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
-                             int dtype, int op, hipStream_t stream, const int *guard) {
+                             int dtype, int op, hipStream_t stream, const int *guard,
+                             const void *const *table) {
   if (count == 0) return hipSuccess;
   if (nsrc < 1 || nsrc > kMaxReduceSources) return hipErrorInvalidValue;
   return DispatchType(dtype, op == kOpOr, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;
     switch (op) {
-      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard);
-      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard);
-      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard);
-      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard);
+      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table);
+      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table);
+      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table);
+      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table);
       default: return hipErrorInvalidValue;
     }
   });

@@ -54,9 +54,10 @@ int SliceRanges(size_t begin, size_t size, size_t total, size_t lo[2], size_t hi
 }
 }  // namespace
 
-PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream)
+PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream,
+                     const SymHeapInfo &heap)
     : device_(device), stage_bytes_(RoundUp(std::max<size_t>(stage_bytes, 1 << 20), 1 << 16)),
-      stream_(stream) {
+      stream_(stream), heap_(heap) {
   CheckHip(hipSetDevice(device_), "hipSetDevice");
   void *p = nullptr;
   // uncached: peers poll the flags and stream the stage buffers over xGMI; nothing of it may
@@ -75,6 +76,11 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
   local_.stage_bytes = stage_bytes_;
   local_.pid = static_cast<int32_t>(getpid());
   local_.device = device_;
+  local_.heap_bytes = heap_.base != nullptr ? heap_.bytes : 0;
+  std::memcpy(local_.heap_ipc, heap_.ipc, sizeof(local_.heap_ipc));
+  void *tbl = nullptr;
+  CheckHip(hipMalloc(&tbl, kMaxPeers * sizeof(void *)), "hipMalloc(source table)");
+  table_ = static_cast<const void **>(tbl);
   void *hw = nullptr;
   CheckHip(hipHostMalloc(&hw, 64, hipHostMallocCoherent | hipHostMallocMapped),
            "hipHostMalloc(peer words)");
@@ -93,6 +99,12 @@ PeerGroup::~PeerGroup() {
   for (size_t r = 0; r < peer_base_.size(); ++r) {
     if (peer_base_[r] != nullptr && peer_base_[r] != base_) (void)hipIpcCloseMemHandle(peer_base_[r]);
   }
+  for (size_t r = 0; r < peer_heap_.size(); ++r) {
+    if (peer_heap_[r] != nullptr && peer_heap_[r] != heap_.base) {
+      (void)hipIpcCloseMemHandle(peer_heap_[r]);
+    }
+  }
+  if (table_ != nullptr) (void)hipFree(const_cast<void **>(table_));
   if (base_ != nullptr) (void)hipFree(base_);
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
 }
@@ -131,6 +143,25 @@ bool PeerGroup::Open(const std::vector<PeerRecord> &all, int rank, std::string *
     }
     peer_base_[r] = static_cast<char *>(p);
   }
+  peer_heap_.assign(n, nullptr);
+  for (int r = 0; r < n; ++r) {
+    if (all[r].heap_bytes == 0) continue;
+    if (r == rank) {
+      peer_heap_[r] = heap_.base;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, all[r].heap_ipc, sizeof(h));
+    void *p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      *why = std::string("hipIpcOpenMemHandle(heap of rank ") + std::to_string(r) +
+             "): " + hipGetErrorString(e);
+      return false;
+    }
+    peer_heap_[r] = static_cast<char *>(p);
+  }
   n_ = n;
   rank_ = rank;
   opened_ = true;
@@ -151,14 +182,14 @@ bool PeerGroup::failed() const {
   return host_words_ != nullptr && __atomic_load_n(&host_words_[1], __ATOMIC_SEQ_CST) != 0;
 }
 
-hipError_t PeerGroup::Barrier() {
+hipError_t PeerGroup::Barrier(const ResolveArgs *resolve) {
   PeerFlagTable t;
   for (int p = 0; p < kMaxPeers; ++p) {
     t.p[p] = p < n_ ? reinterpret_cast<unsigned long long *>(peer_base_[p]) : nullptr;
   }
   ++epoch_;
   return LaunchPeerBarrier(t, rank_, n_, epoch_, &host_words_[0], dev_status(), &host_words_[1],
-                           deadline_ticks_, stream_);
+                           deadline_ticks_, resolve, stream_);
 }
 
 #define XRABIT_TRY_HIP(expr)              \
@@ -170,20 +201,22 @@ hipError_t PeerGroup::Barrier() {
 hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_t count,
                                 int dtype, int op, int prep, double alpha) {
   ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
-                                const int *guard, hipStream_t st) {
-    return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard);
+                                const int *guard, const void *const *table, hipStream_t st) {
+    return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table);
   };
-  return AllreduceImpl(send, recv, recv2, count, ElemBytes(dtype), dtype, prep, alpha, step);
+  return AllreduceImpl(send, recv, recv2, count, ElemBytes(dtype), dtype, prep, alpha, step,
+                       true);
 }
 
 hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                                       size_t type_nbytes, const ReduceStep &step) {
-  return AllreduceImpl(send, recv, recv2, count, type_nbytes, -1, kPrepCopy, 1.0, step);
+  // user reductions take host-computed source pointers: every rank stages its input
+  return AllreduceImpl(send, recv, recv2, count, type_nbytes, -1, kPrepCopy, 1.0, step, false);
 }
 
 hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, size_t count,
                                     size_t tn, int dtype, int prep, double alpha,
-                                    const ReduceStep &step) {
+                                    const ReduceStep &step, bool indirect) {
   utils::Assert(opened_, "peer group not opened");
   // segments are multiples of 256 elements: 256-byte aligned for any element size
   const size_t quantum = 256 * static_cast<size_t>(n_);
@@ -201,22 +234,47 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     const int which = parity_;
     parity_ ^= 1;
     char *mine = stage(rank_, which);
+    const char *chunk_src = in + off * tn;
+    // zero copy: an input in the symmetric heap is read in place by the peers (its location
+    // goes out in this rank's mailbox; each rank decides for itself)
+    const bool zero_copy = indirect && prep == kPrepCopy && InHeap(chunk_src, c * tn) &&
+                           (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
     XRABIT_TRY_HIP(mark(0));
-    if (prep == kPrepCopy) {
-      XRABIT_TRY_HIP(LaunchCopy(mine, in + off * tn, c * tn, stream_));
+    if (zero_copy) {
+      ++zero_copy_chunks_;
+    } else if (prep == kPrepCopy) {
+      XRABIT_TRY_HIP(LaunchCopy(mine, chunk_src, c * tn, stream_));
     } else {
-      XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, in + off * tn, c, dtype, prep, alpha, stream_));
+      XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, chunk_src, c, dtype, prep, alpha, stream_));
     }
     XRABIT_TRY_HIP(mark(1));
-    XRABIT_TRY_HIP(Barrier());
-    XRABIT_TRY_HIP(mark(2));
     const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
     SegRange(c, seg, rank_, &lo, &hi);
+    if (indirect) {
+      ResolveArgs ra{};
+      ra.my_mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(
+                                                      chunk_src - heap_.base))
+                                : static_cast<unsigned long long>(mine - base_);
+      ra.parity = which;
+      for (int p = 0; p < n_; ++p) {
+        ra.stage_base[p] = peer_base_[p];
+        ra.heap_base[p] = peer_heap_.empty() ? nullptr : peer_heap_[p];
+      }
+      ra.seg_off = lo * tn;
+      ra.table = table_;
+      XRABIT_TRY_HIP(Barrier(&ra));
+    } else {
+      XRABIT_TRY_HIP(Barrier());
+    }
+    XRABIT_TRY_HIP(mark(2));
     if (hi > lo) {
       const void *srcs[kMaxPeers];
+      // host pointers: the staged locations (the table, when used, holds the real ones; both
+      // are 256-byte aligned)
       for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which) + lo * tn;  // rank order: identical
-      XRABIT_TRY_HIP(step(mine + lo * tn, srcs, n_, hi - lo, dev_status(), stream_));
+      XRABIT_TRY_HIP(step(mine + lo * tn, srcs, n_, hi - lo, dev_status(),
+                          indirect ? table_ : nullptr, stream_));
     }
     XRABIT_TRY_HIP(mark(3));
     XRABIT_TRY_HIP(Barrier());

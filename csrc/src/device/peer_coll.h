@@ -45,6 +45,11 @@ constexpr int kMaxCopySegs = 16;
  *  flags at offset 0, the local failure word at kPeerStatusOffset */
 constexpr size_t kPeerFlagBytes = 64 * 1024;
 constexpr size_t kPeerStatusOffset = 4096;
+/*! \brief two mailbox words (by stage parity): where this rank's input of the current chunk
+ *  lives, published before the first barrier of the chunk (see ResolveArgs) */
+constexpr size_t kPeerMailboxOffset = 8192;
+/*! \brief mailbox flag: the offset is into the symmetric heap, not the stage allocation */
+constexpr unsigned long long kMailboxHeap = 1ull << 63;
 
 struct PeerFlagTable {
   unsigned long long *p[kMaxPeers];
@@ -63,9 +68,26 @@ struct CopyBatch {
   const int *guard;  // optional device word: the launch does nothing when it is non-zero
 };
 
+/*!
+ * \brief optional work of a chunk's first barrier: publish where this rank's input is (its
+ *        mailbox word) before signalling, and after the wait turn every peer's mailbox into a
+ *        source pointer for this rank's segment (table[p] = base_p + offset_p + seg_off) in
+ *        cached device memory, so the reduce kernel reads n scalars instead of n remote words
+ *        per workgroup.
+ */
+struct ResolveArgs {
+  unsigned long long my_mailbox;    // value to publish
+  int parity;                       // mailbox slot
+  const char *stage_base[kMaxPeers];
+  const char *heap_base[kMaxPeers];  // nullptr: that peer has no symmetric heap
+  size_t seg_off;                   // byte offset of this rank's segment in the chunk
+  const void **table;               // out: n source pointers
+};
+
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
                              const volatile int *abort_word, int *dev_status, int *host_status,
-                             long long deadline_ticks, hipStream_t stream);
+                             long long deadline_ticks, const ResolveArgs *resolve,
+                             hipStream_t stream);
 hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream);
 
 /*! \brief fixed-size record every rank contributes when a group is built */
@@ -76,12 +98,22 @@ struct PeerRecord {
   uint64_t stage_bytes;
   int32_t pid;
   int32_t device;
+  char heap_ipc[64];   // hipIpcMemHandle_t of the symmetric heap (heap_bytes != 0)
+  uint64_t heap_bytes;
+};
+
+/*! \brief this rank's symmetric heap (owned by the DevicePlane, outlives peer groups) */
+struct SymHeapInfo {
+  char *base{nullptr};
+  size_t bytes{0};
+  char ipc[64]{};
 };
 
 class PeerGroup {
  public:
   /*! \brief allocate and export the local buffers; stage_bytes per stage buffer */
-  PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream);
+  PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStream_t stream,
+            const SymHeapInfo &heap = SymHeapInfo());
   ~PeerGroup();
   PeerGroup(const PeerGroup &) = delete;
   PeerGroup &operator=(const PeerGroup &) = delete;
@@ -102,7 +134,8 @@ class PeerGroup {
   /*! \brief reduction step of a custom allreduce: dst = reduce(srcs[0..n)) over count
    *  elements on `stream`, doing nothing when *guard != 0 */
   typedef std::function<hipError_t(void *dst, const void *const *srcs, int n, size_t count,
-                                   const int *guard, hipStream_t stream)>
+                                   const int *guard, const void *const *table,
+                                   hipStream_t stream)>
       ReduceStep;
   /*! \brief allreduce of count elements of type_nbytes bytes with a caller-provided reduction */
   hipError_t AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
@@ -116,6 +149,8 @@ class PeerGroup {
   /*! \brief true when a barrier gave up (read after the stream drained) */
   bool failed() const;
   uint64_t barriers() const { return epoch_; }
+  /*! \brief chunks whose input was read in place from the symmetric heap (no stage copy) */
+  uint64_t zero_copy_chunks() const { return zero_copy_chunks_; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
   /*! \brief fold the last timed op into the phase totals (call after the stream drained) */
@@ -128,9 +163,15 @@ class PeerGroup {
   }
 
  private:
-  hipError_t Barrier();
+  hipError_t Barrier(const ResolveArgs *resolve = nullptr);
   hipError_t AllreduceImpl(const void *send, void *recv, void *recv2, size_t count, size_t tn,
-                           int dtype, int prep, double alpha, const ReduceStep &step);
+                           int dtype, int prep, double alpha, const ReduceStep &step,
+                           bool indirect);
+  /*! \brief true if [p, p + bytes) lies in this rank's symmetric heap */
+  bool InHeap(const void *p, size_t bytes) const {
+    const char *c = static_cast<const char *>(p);
+    return heap_.base != nullptr && c >= heap_.base && c + bytes <= heap_.base + heap_.bytes;
+  }
   char *stage(int rank, int which) const;
   int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
   void NewBatch(CopyBatch *b) const {
@@ -145,6 +186,9 @@ class PeerGroup {
   int clock_khz_{100000};
   char *base_{nullptr};                 // local allocation
   std::vector<char *> peer_base_;       // mapped allocations (own = base_)
+  SymHeapInfo heap_;                    // own symmetric heap (not owned)
+  std::vector<char *> peer_heap_;       // mapped heaps (own = heap_.base), nullptr if none
+  const void **table_{nullptr};         // device table of resolved reduce sources
   int *host_words_{nullptr};            // pinned: [0] abort, [1] status
   int n_{0}, rank_{0};
   unsigned long long epoch_{0};
@@ -155,6 +199,7 @@ class PeerGroup {
   hipEvent_t ev_[kPhases + 1]{};
   double phase_ms_[kPhases]{};
   uint64_t timed_ops_{0};
+  uint64_t zero_copy_chunks_{0};
 };
 
 }  // namespace device

@@ -32,14 +32,28 @@ constexpr int kBlock = 256;
 constexpr int kUnroll = 1;  // 4 KiB tiles: as for the streaming kernels of kernels.hip
 constexpr size_t kTileBytes = static_cast<size_t>(kBlock) * kUnroll * 16;
 
+template <bool RESOLVE>
 __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int rank, int n,
                                                         unsigned long long epoch,
                                                         const volatile int *abort_word,
                                                         int *dev_status, int *host_status,
-                                                        long long deadline_ticks) {
+                                                        long long deadline_ticks,
+                                                        ResolveArgs resolve) {
   const int t = threadIdx.x;
   // an earlier barrier of this group failed: stay failed, signal nothing
   if (__hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  auto mailbox = [&](int p) {
+    return reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(flags.p[p]) +
+                                                  kPeerMailboxOffset) +
+           resolve.parity;
+  };
+  if (RESOLVE) {
+    if (t == 0) {
+      __hip_atomic_store(mailbox(rank), resolve.my_mailbox, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();  // the mailbox store precedes every lane's flag store below
+  }
   // make the bytes written by earlier kernels of this stream visible before signalling
   __threadfence_system();
   if (t < n) {
@@ -56,6 +70,15 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
     }
   }
   __threadfence_system();
+  if (RESOLVE) {
+    __syncthreads();
+    if (t < n && __hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+      const unsigned long long m =
+          __hip_atomic_load(mailbox(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const char *base = (m & kMailboxHeap) != 0 ? resolve.heap_base[t] : resolve.stage_base[t];
+      resolve.table[t] = base + (m & ~kMailboxHeap) + resolve.seg_off;
+    }
+  }
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -123,10 +146,17 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
 
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
                              const volatile int *abort_word, int *dev_status, int *host_status,
-                             long long deadline_ticks, hipStream_t stream) {
+                             long long deadline_ticks, const ResolveArgs *resolve,
+                             hipStream_t stream) {
   if (n < 1 || n > kMaxPeers || rank < 0 || rank >= n) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(PeerBarrierKernel, dim3(1), dim3(64), 0, stream, flags, rank, n, epoch,
-                     abort_word, dev_status, host_status, deadline_ticks);
+  if (resolve != nullptr) {
+    hipLaunchKernelGGL(PeerBarrierKernel<true>, dim3(1), dim3(64), 0, stream, flags, rank, n,
+                       epoch, abort_word, dev_status, host_status, deadline_ticks, *resolve);
+  } else {
+    ResolveArgs none{};
+    hipLaunchKernelGGL(PeerBarrierKernel<false>, dim3(1), dim3(64), 0, stream, flags, rank, n,
+                       epoch, abort_word, dev_status, host_status, deadline_ticks, none);
+  }
   return hipGetLastError();
 }
 

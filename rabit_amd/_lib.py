@@ -87,6 +87,7 @@ def _declare(d: ctypes.CDLL) -> None:
         "RabitDevChecksum": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
         "RabitDevFill": (c_int, [c_void_p, c_size_t, c_int, c_double, c_void_p]),
         "RabitDevCopy": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+        "RabitDevSymmetricAlloc": (c_void_p, [c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(d, name)

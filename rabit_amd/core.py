@@ -392,6 +392,43 @@ def set_error_mode(raise_errors: bool):
     _LIB.RabitSetErrorMode(1 if raise_errors else 0)
 
 
+class _DeviceArray:
+    """__cuda_array_interface__ view of engine-owned HBM (torch.as_tensor wraps it zero-copy)."""
+
+    def __init__(self, ptr: int, shape, typestr: str, owner):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr,
+                                         "data": (ptr, False), "version": 2, "strides": None}
+        self._owner = owner
+
+
+def symmetric_empty(shape, dtype=None):
+    """A torch tensor in the engine's symmetric heap (init with rabit_device_symmetric_heap=...).
+
+    Peers map this memory through IPC, so allreducing a tensor allocated here skips the staging
+    copy of the direct transport.  The memory belongs to the engine (valid until finalize())."""
+    import torch
+
+    _check_init()
+    dtype = dtype or torch.float32
+    if isinstance(shape, int):
+        shape = (shape,)
+    numel = 1
+    for d in shape:
+        numel *= int(d)
+    esize = torch.empty((), dtype=dtype).element_size()
+    ptr = _LIB.RabitDevSymmetricAlloc(max(1, numel * esize))
+    if not ptr:
+        raise MemoryError("symmetric heap unavailable or full (rabit_device_symmetric_heap)")
+    typestr = {torch.float32: "<f4", torch.float64: "<f8", torch.int32: "<i4",
+               torch.int64: "<i8", torch.uint8: "|u1", torch.int8: "|i1",
+               torch.float16: "<f2"}[dtype]
+    dev = torch.device("cuda", get_device())
+    with torch.cuda.device(dev):
+        t = torch.as_tensor(_DeviceArray(ptr, shape, typestr, None), device=dev)
+    assert t.data_ptr() == ptr, "torch copied the symmetric buffer"
+    return t
+
+
 def lib():
     """The loaded ctypes library (for rabit_amd.ops)."""
     return _LIB

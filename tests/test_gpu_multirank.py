@@ -60,3 +60,12 @@ def test_calibration_flow():
     rc, out = _run("calibrate_check.py", 3)
     assert rc == 0, out[-5000:]
     assert out.count("CALIB OK") == 3, out[-3000:]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_symmetric_zero_copy(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("symmetric_check.py", world)
+    assert rc == 0, out[-5000:]
+    assert out.count("SYMMETRIC OK") == world, out[-3000:]

@@ -10,6 +10,7 @@ phases of an 8-GPU run (reduce, gather) are not represented.  Rank 0 prints one 
 size with the median op time and the average hipEvent time of each phase.
 """
 import json
+import os
 import sys
 import time
 
@@ -20,12 +21,21 @@ import rabit_amd as rabit
 
 
 def main():
+    sym = os.environ.get("XR_SYM", "0") == "1"
     rabit.init(sys.argv[1:], lib="base", rabit_device=0, rabit_device_phase_timing=1,
-               rabit_device_algo="direct")
+               rabit_device_algo="direct",
+               **({"rabit_device_symmetric_heap": "160M"} if sym else {}))
     rank, world = rabit.get_rank(), rabit.get_world_size()
     dev = torch.device("cuda", 0)
-    for nbytes in (256 << 10, 1 << 20, 8 << 20, 32 << 20, 128 << 20):
-        x = torch.ones(nbytes // 4, device=dev)
+    sizes = (256 << 10, 1 << 20, 8 << 20, 32 << 20, 128 << 20)
+    if sym:
+        sizes = (1 << 20, 8 << 20, 128 << 20)  # bump-allocated heap: keep the total small
+    for nbytes in sizes:
+        if sym:
+            x = rabit.symmetric_empty(nbytes // 4)
+            x.fill_(1.0)
+        else:
+            x = torch.ones(nbytes // 4, device=dev)
         for _ in range(3):
             rabit.allreduce(x, rabit.SUM)
         times = []
@@ -48,7 +58,7 @@ def main():
         med = float(rabit.allreduce(np.array([med]), rabit.MAX)[0])
         if rank == 0:
             print(json.dumps({
-                "world_on_one_gpu": world, "bytes": nbytes, "t_us": round(med * 1e6, 1),
+                "world_on_one_gpu": world, "bytes": nbytes, "symmetric": sym, "t_us": round(med * 1e6, 1),
                 "phase_us": phase, "timed_ops": n1 - n0,
             }), flush=True)
         del x
