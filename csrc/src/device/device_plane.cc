@@ -425,8 +425,8 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   if (!RcclOp(op, &o)) {
     PeerGroup::ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
                                              const int *guard, const void *const *table,
-                                             hipStream_t st) {
-      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table);
+                                             double post, hipStream_t st) {
+      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table, post);
     };
     Status s = AllreduceByKernel(send, recv, count, TypeBytes(dtype), step, probe);
     if (s != Status::kSuccess) return s;
@@ -447,7 +447,7 @@ Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, s
                                     size_t type_nbytes, DeviceReduceLauncher *launcher,
                                     const FailureProbe &probe) {
   PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
-                                          const int *guard, const void *const *,
+                                          const int *guard, const void *const *, double,
                                           hipStream_t st) {
     return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
   };
@@ -504,7 +504,7 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
       srcs.push_back(b + static_cast<size_t>(done) * seg_bytes);
       ++done;
     }
-    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, nullptr,
+    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, nullptr, 0.0,
                   stream_),
              "allreduce reduce step");
   }

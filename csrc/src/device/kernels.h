@@ -31,11 +31,13 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
  *        source).  guard: optional device word; the launch does nothing when it is non-zero
  *        (set by a failed peer barrier earlier on the stream).  table: optional device array of
  *        nsrc source pointers written by an earlier kernel (srcs then only serve the host-side
- *        alignment check and must be aligned like the table's pointers).
+ *        alignment check and must be aligned like the table's pointers).  post_scale != 0
+ *        multiplies the reduced value (float/double only): the averaging of a data-parallel
+ *        gradient applied once after the sum, so the inputs can be read unmodified.
  */
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard = nullptr,
-                             const void *const *table = nullptr);
+                             const void *const *table = nullptr, double post_scale = 0.0);
 /*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);

@@ -146,11 +146,36 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <typename T>
+__device__ __forceinline__ T PrepApply(T x, int prep, T alpha) {
+  switch (prep) {
+    case kPrepSquare: return x * x;
+    case kPrepScale: return x * alpha;
+    case kPrepAbs:
+      if constexpr (std::is_signed<T>::value) return x < T(0) ? T(0) - x : x;
+      return x;
+    default: return x;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 PrepVec(uint4 v, int prep, T alpha) {
+  constexpr int L = 16 / sizeof(T);
+  T x[L];
+  __builtin_memcpy(x, &v, 16);
+#pragma unroll
+  for (int j = 0; j < L; ++j) x[j] = PrepApply<T>(x[j], prep, alpha);
+  uint4 r;
+  __builtin_memcpy(&r, x, 16);
+  return r;
+}
+
 // ---------------------------------------------------------------- multi-source reduce
 struct SrcList {
   const void *p[kMaxReduceSources];
   const int *guard;  // optional: skip the whole launch when *guard != 0 (failed peer barrier)
   const void *const *table;  // optional: device table of source pointers (overrides p)
+  double post_scale;         // != 0: multiply the reduced value by it (floating types)
 };
 
 /*! \brief source k: from the device table when given (written by an earlier kernel, e.g. a
@@ -182,6 +207,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       uint4 acc = x[0][u];
 #pragma unroll
       for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, x[k][u]);
+      if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
       StoreNT(d + base + u * kBlock, acc);
     }
   } else {
@@ -192,6 +218,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       for (int k = 1; k < NSRC; ++k) {
         acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(Src(srcs, k))[i]);
       }
+      if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
       StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
     }
   }
@@ -199,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     T acc = static_cast<const T *>(Src(srcs, 0))[i];
 #pragma unroll
     for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
+    if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
     dst[i] = acc;
   });
 }
@@ -210,6 +238,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcLis
   if (i >= n || Guarded(srcs.guard)) return;
   T acc = static_cast<const T *>(Src(srcs, 0))[i];
   for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
+  if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
   dst[i] = acc;
 }
 
@@ -223,10 +252,11 @@ void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
 
 template <typename T, int OP>
 hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st,
-                       const int *guard, const void *const *table) {
+                       const int *guard, const void *const *table, double post_scale) {
   SrcList sl;
   sl.guard = guard;
   sl.table = table;
+  sl.post_scale = post_scale;
   bool aligned = Aligned16(dst);
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;
@@ -253,30 +283,6 @@ hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, h
 }
 
 // ---------------------------------------------------------------- lazy prepare
-template <typename T>
-__device__ __forceinline__ T PrepApply(T x, int prep, T alpha) {
-  switch (prep) {
-    case kPrepSquare: return x * x;
-    case kPrepScale: return x * alpha;
-    case kPrepAbs:
-      if constexpr (std::is_signed<T>::value) return x < T(0) ? T(0) - x : x;
-      return x;
-    default: return x;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ uint4 PrepVec(uint4 v, int prep, T alpha) {
-  constexpr int L = 16 / sizeof(T);
-  T x[L];
-  __builtin_memcpy(x, &v, 16);
-#pragma unroll
-  for (int j = 0; j < L; ++j) x[j] = PrepApply<T>(x[j], prep, alpha);
-  uint4 r;
-  __builtin_memcpy(&r, x, 16);
-  return r;
-}
-
 template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void PrepareTileKernel(T *dst, T *dst2, const T *src,
                                                             size_t n, int prep, T alpha) {
@@ -476,7 +482,7 @@ struct OrTag {
   static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st,
                             const int *guard, const void *const *table) {
     if constexpr (std::is_integral<T>::value) {
-      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table);
+      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table, 0.0);
     }
     return hipErrorInvalidValue;
   }
@@ -500,15 +506,16 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard,
-                             const void *const *table) {
+                             const void *const *table, double post_scale) {
   if (count == 0) return hipSuccess;
+  if (post_scale != 0.0 && dtype != 6 && dtype != 7) return hipErrorInvalidValue;  // float/double
   if (nsrc < 1 || nsrc > kMaxReduceSources) return hipErrorInvalidValue;
   return DispatchType(dtype, op == kOpOr, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;
     switch (op) {
-      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table);
-      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table);
-      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table);
+      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
+      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
+      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
       case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table);
       default: return hipErrorInvalidValue;
     }

@@ -201,11 +201,12 @@ hipError_t PeerGroup::Barrier(const ResolveArgs *resolve) {
 hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_t count,
                                 int dtype, int op, int prep, double alpha) {
   ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
-                                const int *guard, const void *const *table, hipStream_t st) {
-    return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table);
+                                const int *guard, const void *const *table, double post,
+                                hipStream_t st) {
+    return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table, post);
   };
   return AllreduceImpl(send, recv, recv2, count, ElemBytes(dtype), dtype, prep, alpha, step,
-                       true);
+                       true, op == 2);
 }
 
 hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
@@ -216,7 +217,7 @@ hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2,
 
 hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, size_t count,
                                     size_t tn, int dtype, int prep, double alpha,
-                                    const ReduceStep &step, bool indirect) {
+                                    const ReduceStep &step, bool indirect, bool op_is_sum) {
   utils::Assert(opened_, "peer group not opened");
   // segments are multiples of 256 elements: 256-byte aligned for any element size
   const size_t quantum = 256 * static_cast<size_t>(n_);
@@ -226,6 +227,10 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   const char *in = static_cast<const char *>(send);
   char *out = static_cast<char *>(recv);
   char *out2 = static_cast<char *>(recv2);
+  // sum(a x_p) = a sum(x_p): exact reordering only for the linear op
+  const bool post_scale =
+      indirect && op_is_sum && prep == kPrepScale && (dtype == 6 || dtype == 7);
+  const int stage_prep = post_scale ? kPrepCopy : prep;
   // per-phase timing of single-chunk ops (rabit_device_phase_timing=1)
   const bool timed = timing_ && count <= chunk;
   auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
@@ -236,16 +241,19 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     char *mine = stage(rank_, which);
     const char *chunk_src = in + off * tn;
     // zero copy: an input in the symmetric heap is read in place by the peers (its location
-    // goes out in this rank's mailbox; each rank decides for itself)
-    const bool zero_copy = indirect && prep == kPrepCopy && InHeap(chunk_src, c * tn) &&
+    // goes out in this rank's mailbox; each rank decides for itself).  A floating-point scale
+    // (gradient averaging) is applied once after the sum on every rank, so inputs stay raw.
+    const bool zero_copy = indirect && stage_prep == kPrepCopy &&
+                           InHeap(chunk_src, c * tn) &&
                            (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
     XRABIT_TRY_HIP(mark(0));
     if (zero_copy) {
       ++zero_copy_chunks_;
-    } else if (prep == kPrepCopy) {
+    } else if (stage_prep == kPrepCopy) {
       XRABIT_TRY_HIP(LaunchCopy(mine, chunk_src, c * tn, stream_));
     } else {
-      XRABIT_TRY_HIP(LaunchPrepare(mine, nullptr, chunk_src, c, dtype, prep, alpha, stream_));
+      XRABIT_TRY_HIP(
+          LaunchPrepare(mine, nullptr, chunk_src, c, dtype, stage_prep, alpha, stream_));
     }
     XRABIT_TRY_HIP(mark(1));
     const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
@@ -274,7 +282,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       // are 256-byte aligned)
       for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which) + lo * tn;  // rank order: identical
       XRABIT_TRY_HIP(step(mine + lo * tn, srcs, n_, hi - lo, dev_status(),
-                          indirect ? table_ : nullptr, stream_));
+                          indirect ? table_ : nullptr, post_scale ? alpha : 0.0, stream_));
     }
     XRABIT_TRY_HIP(mark(3));
     XRABIT_TRY_HIP(Barrier());

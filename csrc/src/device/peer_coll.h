@@ -135,7 +135,7 @@ class PeerGroup {
    *  elements on `stream`, doing nothing when *guard != 0 */
   typedef std::function<hipError_t(void *dst, const void *const *srcs, int n, size_t count,
                                    const int *guard, const void *const *table,
-                                   hipStream_t stream)>
+                                   double post_scale, hipStream_t stream)>
       ReduceStep;
   /*! \brief allreduce of count elements of type_nbytes bytes with a caller-provided reduction */
   hipError_t AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
@@ -166,7 +166,7 @@ class PeerGroup {
   hipError_t Barrier(const ResolveArgs *resolve = nullptr);
   hipError_t AllreduceImpl(const void *send, void *recv, void *recv2, size_t count, size_t tn,
                            int dtype, int prep, double alpha, const ReduceStep &step,
-                           bool indirect);
+                           bool indirect, bool op_is_sum = false);
   /*! \brief true if [p, p + bytes) lies in this rank's symmetric heap */
   bool InHeap(const void *p, size_t bytes) const {
     const char *c = static_cast<const char *>(p);

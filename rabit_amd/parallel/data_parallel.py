@@ -19,11 +19,16 @@ class GradientBuckets:
     skipped together with the reduction when the result is replayed after a failure.
     """
 
-    def __init__(self, params: Iterable, bucket_mb: float = 256.0, average: bool = True):
+    def __init__(self, params: Iterable, bucket_mb: float = 256.0, average: bool = True,
+                 symmetric: bool = False):
         import torch
 
         self.params = [p for p in params if p.requires_grad]
         self.average = average
+        # symmetric=True: HBM buckets come from the engine's symmetric heap (init with
+        # rabit_device_symmetric_heap), so the direct transport reduces them in place without a
+        # staging copy; the heap is uncached, which the gradient-producing kernels also see
+        self.symmetric = symmetric
         cap = max(1, int(bucket_mb * (1 << 20)))
         self.buckets: List["torch.Tensor"] = []
         self._groups: List[List] = []
@@ -45,7 +50,11 @@ class GradientBuckets:
     def _make_bucket(self, plist, size, dev, dtype):
         import torch
 
-        flat = torch.zeros(size, dtype=dtype, device=dev)
+        if self.symmetric and dev.type == "cuda":
+            flat = rabit.symmetric_empty(size, dtype)
+            flat.zero_()
+        else:
+            flat = torch.zeros(size, dtype=dtype, device=dev)
         off = 0
         for p in plist:
             n = p.numel()

@@ -69,3 +69,12 @@ def test_symmetric_zero_copy(world):
     rc, out = _run("symmetric_check.py", world)
     assert rc == 0, out[-5000:]
     assert out.count("SYMMETRIC OK") == world, out[-3000:]
+
+
+@pytest.mark.parametrize("sym", ["0", "1"])
+def test_gradient_buckets(sym):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("buckets_check.py", 2, [sym])
+    assert rc == 0, out[-5000:]
+    assert out.count("BUCKETS OK") == 2, out[-3000:]
