@@ -257,6 +257,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_.reset(
         new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_, heap_));
     if (cfg_.phase_timing) peers_->EnableTiming();
+    peers_->set_oneshot_max(cfg_.oneshot_max);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();

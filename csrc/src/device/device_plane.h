@@ -50,6 +50,7 @@ struct DeviceConfig {
   bool phase_timing{false};            // direct transport: hipEvent timing of each phase
   bool ops_on_user_stream{true};       // enqueue collectives on the caller's stream
   size_t sym_heap{0};                  // bytes of the symmetric (IPC-exported) heap, 0: none
+  size_t oneshot_max{256u << 10};      // direct allreduce: one-shot up to this many bytes
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -149,6 +150,7 @@ class DevicePlane {
   const SymHeapInfo &sym_heap() const { return heap_; }
   size_t sym_heap_used() const { return heap_used_; }
   uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
+  uint64_t oneshot_ops() const { return peers_ ? peers_->oneshot_ops() : 0; }
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;
 

@@ -243,7 +243,11 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     // zero copy: an input in the symmetric heap is read in place by the peers (its location
     // goes out in this rank's mailbox; each rank decides for itself).  A floating-point scale
     // (gradient averaging) is applied once after the sum on every rank, so inputs stay raw.
-    const bool zero_copy = indirect && stage_prep == kPrepCopy &&
+    // One-shot ops never read in place: with a single barrier nothing would stop this rank
+    // from overwriting its input (second destination, the caller's next kernels) while a slower
+    // peer is still reading it.  Two-shot reads all inputs before the second barrier.
+    const bool oneshot = indirect && c * tn <= oneshot_max_ && count <= chunk;
+    const bool zero_copy = indirect && !oneshot && stage_prep == kPrepCopy &&
                            InHeap(chunk_src, c * tn) &&
                            (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
     XRABIT_TRY_HIP(mark(0));
@@ -256,6 +260,39 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
           LaunchPrepare(mine, nullptr, chunk_src, c, dtype, stage_prep, alpha, stream_));
     }
     XRABIT_TRY_HIP(mark(1));
+    if (oneshot) {
+      // one-shot (small ops): one barrier, then every rank reduces the whole chunk from all
+      // peers' inputs itself, in rank order (identical results everywhere), straight into the
+      // destination — no second barrier, no gather
+      ResolveArgs ra{};
+      ra.my_mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(
+                                                      chunk_src - heap_.base))
+                                : static_cast<unsigned long long>(mine - base_);
+      ra.parity = which;
+      for (int p = 0; p < n_; ++p) {
+        ra.stage_base[p] = peer_base_[p];
+        ra.heap_base[p] = peer_heap_.empty() ? nullptr : peer_heap_[p];
+      }
+      ra.seg_off = 0;
+      ra.table = table_;
+      XRABIT_TRY_HIP(Barrier(&ra));
+      XRABIT_TRY_HIP(mark(2));
+      const void *srcs[kMaxPeers];
+      for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which);
+      XRABIT_TRY_HIP(step(out + off * tn, srcs, n_, c, dev_status(), table_,
+                          post_scale ? alpha : 0.0, stream_));
+      XRABIT_TRY_HIP(mark(3));
+      XRABIT_TRY_HIP(mark(4));  // (no second barrier)
+      if (out2 != nullptr) {
+        CopyBatch b;
+        NewBatch(&b);
+        AddSeg(&b, out2 + off * tn, out + off * tn, nullptr, c * tn);
+        XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+      }
+      XRABIT_TRY_HIP(mark(5));
+      ++oneshot_ops_;
+      continue;
+    }
     const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
     SegRange(c, seg, rank_, &lo, &hi);

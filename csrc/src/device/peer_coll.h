@@ -151,6 +151,9 @@ class PeerGroup {
   uint64_t barriers() const { return epoch_; }
   /*! \brief chunks whose input was read in place from the symmetric heap (no stage copy) */
   uint64_t zero_copy_chunks() const { return zero_copy_chunks_; }
+  /*! \brief ops of at most this many bytes use the one-shot allreduce (one barrier) */
+  void set_oneshot_max(size_t b) { oneshot_max_ = b; }
+  uint64_t oneshot_ops() const { return oneshot_ops_; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
   /*! \brief fold the last timed op into the phase totals (call after the stream drained) */
@@ -200,6 +203,8 @@ class PeerGroup {
   double phase_ms_[kPhases]{};
   uint64_t timed_ops_{0};
   uint64_t zero_copy_chunks_{0};
+  size_t oneshot_max_{256u << 10};
+  uint64_t oneshot_ops_{0};
 };
 
 }  // namespace device

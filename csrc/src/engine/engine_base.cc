@@ -90,6 +90,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
+  if (is("rabit_device_oneshot_max")) dcfg_.oneshot_max = core::ParseUnit(name, val);
   if (is("rabit_device_symmetric_heap")) dcfg_.sym_heap = core::ParseUnit(name, val);
   if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
@@ -653,6 +654,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_rccl\":" << (dev_ && dev_->has_comm() ? 1 : 0)
      << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
+     << ",\"oneshot_ops\":" << (dev_ ? dev_->oneshot_ops() : 0)
      << ",\"symmetric_heap_used\":" << (dev_ ? dev_->sym_heap_used() : 0)
      << ",\"device_direct_min\":"
      << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)

@@ -94,7 +94,13 @@ class LocalJob:
             t.join(None if deadline is None else max(0.0, deadline - time.time()))
         if any(t.is_alive() for t in threads):
             self.kill()
-            raise TimeoutError("rabit job did not finish within %s s" % self.timeout)
+            tail = ""
+            if self.capture:
+                for t in threads:
+                    t.join(5)
+                tail = "\n".join("--- worker %d ---\n%s" % (i, "".join(o[-40:]))
+                                 for i, o in enumerate(self.outputs))
+            raise TimeoutError("rabit job did not finish within %s s\n%s" % (self.timeout, tail))
         failed = [rc for rc in self.returncodes if rc != 0]
         if not failed:
             self.tracker.join(30)
