@@ -8,7 +8,9 @@ import rabit_amd as rabit
 from rabit_amd.parallel.data_parallel import GradientBuckets
 
 sym = sys.argv[1] == "1"
-rabit.init(sys.argv[2:], lib="standard", rabit_device=0,
+# two-shot for every bucket (one-shot ops never read their input in place), so the symmetric
+# buckets exercise the zero-copy path
+rabit.init(sys.argv[2:], lib="standard", rabit_device=0, rabit_device_oneshot_max=0,
            **({"rabit_device_symmetric_heap": "64M"} if sym else {}))
 rank, world = rabit.get_rank(), rabit.get_world_size()
 dev = torch.device("cuda", 0)
