@@ -48,6 +48,30 @@ def _timed(rabit, torch, fn, reps, settle=0.0, device_wide=True):
     return float(rabit.allreduce(np.array([med]), rabit.MAX)[0])
 
 
+def reference_measured(world, value):
+    """The reference's own speed_test built from its sources and run on the host of an MI355X
+    box (tools/refbuild/, profiles/r1_h2h_reference/): its Sum time for the same 128 MiB float32
+    job at this world size, as the same whole-job aggregate.  BASELINE.md publishes no number,
+    so `vs_baseline` stays null; this is a measured comparison with its provenance."""
+    path = os.path.join(ROOT, "profiles", "r1_h2h_reference", "h2h_128MiB.jsonl")
+    try:
+        rows = [json.loads(l) for l in open(path) if l.strip()]
+    except OSError:
+        return None
+    for r in rows:
+        if r.get("impl") == "reference" and r.get("world") == world and r.get("rc") == 0:
+            if world == 1:
+                return {"note": "the reference's robust engine returns without work at world 1",
+                        "source": os.path.relpath(path, ROOT)}
+            t = r["sum_mean_s"] / r["nrep"]
+            ref_value = world * r["bytes"] / t / 1e9
+            return {"value": round(ref_value, 3), "unit": "GB/s", "ms_per_op": round(t * 1e3, 2),
+                    "data_path": "host memory over TCP (its only path)",
+                    "vs_reference_measured": round(value / ref_value, 1),
+                    "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def run_extras(rabit, torch, dev, world):
     """BASELINE.json configs 3 and 4 plus the checkpoint cost of config 5, on this job's ranks
     (result log and checkpoint paths included, as in the headline step)."""
@@ -205,6 +229,7 @@ def main():
                       "direct_min_bytes": st.get("device_direct_min", -1),
                       "calibration_us": st.get("calib_us")},
         "extras": extras,
+        "reference_measured": reference_measured(world, aggregate),
     }
     if rank == 0:
         print(json.dumps(rec), flush=True)
