@@ -147,15 +147,21 @@ def main():
     import rabit_amd as rabit
     from rabit_amd.torchrun import init_from_env
 
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; with fewer GPUs than ranks (a rehearsal of the N>1 launch on a
+    # one-GPU box) ranks share GPUs and the direct IPC transport carries the data (RCCL refuses
+    # two ranks on one GPU), which is flagged in the output
+    ngpu = torch.cuda.device_count()
+    gpu = local_rank % ngpu
+    shared_gpu = ngpu < int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    torch.cuda.set_device(gpu)
     # the rabit tracker lives in rank 0 next to the torchrun master port (rabit_amd.torchrun)
     n = args.size_mb * (1 << 20) // 4
     if args.symmetric < 0:
         args.symmetric = 1 if world > 1 else 0
     heap = {"rabit_device_symmetric_heap": str(n * 4 + (16 << 20))} if args.symmetric else {}
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
-                        rabit_world1_fastpath=0, **heap)
-    dev = torch.device("cuda", local_rank)
+                        rabit_world1_fastpath=0, rabit_device=gpu, **heap)
+    dev = torch.device("cuda", gpu)
 
     def barrier():
         rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
@@ -231,6 +237,8 @@ def main():
         "extras": extras,
         "reference_measured": reference_measured(world, aggregate),
     }
+    if shared_gpu:
+        rec["shared_gpu_rehearsal"] = "%d ranks on %d GPU(s): not an xGMI measurement" % (world, ngpu)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     del x

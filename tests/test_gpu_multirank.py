@@ -78,3 +78,30 @@ def test_gradient_buckets(sym):
     rc, out = _run("buckets_check.py", 2, [sym])
     assert rc == 0, out[-5000:]
     assert out.count("BUCKETS OK") == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_torchrun_shared_gpu(n):
+    """bench.py under torch.distributed.run exactly as the driver launches the N>1 runs (ranks
+    share the box's GPU here, so the direct transport carries the data): the result check
+    passes and rank 0 prints one JSON line."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+                          "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", str(n), "--steps", "3", "--warmup", "1", "--extras", "0"],
+                         capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["transport"]["direct"] == 1, rec
