@@ -137,10 +137,11 @@ inline void Allreduce(DType *sendrecvbuf, size_t count, std::function<void()> pr
 
 template <typename DType>
 inline void Allgather(DType *sendrecvbuf, size_t total_size, size_t slice_begin,
-                      size_t slice_end, size_t size_prev_slice, const char *_file,
+                      size_t size_node_slice, size_t size_prev_slice, const char *_file,
                       const int _line, const char *_caller) {
   engine::GetEngine()->Allgather(sendrecvbuf, total_size * sizeof(DType),
-                                 slice_begin * sizeof(DType), slice_end * sizeof(DType),
+                                 slice_begin * sizeof(DType),
+                                 (slice_begin + size_node_slice) * sizeof(DType),
                                  size_prev_slice * sizeof(DType), _file, _line, _caller);
 }
 

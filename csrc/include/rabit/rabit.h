@@ -74,12 +74,15 @@ inline void Allreduce(DType *sendrecvbuf, size_t count, std::function<void()> pr
                       const char *_file = _FILE, const int _line = _LINE,
                       const char *_caller = _CALLER);
 /*!
- * \brief ring allgather; indices count elements of DType.  This rank owns
- *        [slice_begin, slice_end), the slice of rank+1 starts at slice_end (wrapping)
+ * \brief ring allgather; all sizes count elements of DType.  This rank owns
+ *        [slice_begin, slice_begin + size_node_slice); the slice of rank+1 starts where it
+ *        ends (wrapping).  The 4th argument is a SIZE, as in the reference's implementation
+ *        (include/rabit/internal/rabit-inl.h:202-213, used so by test/model_recover.cc:82);
+ *        the reference's header comment calls it slice_end.
  */
 template <typename DType>
 inline void Allgather(DType *sendrecvbuf_, size_t total_size, size_t slice_begin,
-                      size_t slice_end, size_t size_prev_slice, const char *_file = _FILE,
+                      size_t size_node_slice, size_t size_prev_slice, const char *_file = _FILE,
                       const int _line = _LINE, const char *_caller = _CALLER);
 /*!
  * \brief load the latest checkpoint

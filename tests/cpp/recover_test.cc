@@ -124,7 +124,7 @@ int main(int argc, char *argv[]) {
       const int z = 151 + it;
       std::vector<float> all(n * world);
       for (size_t i = 0; i < n; ++i) all[rank * n + i] = Contrib(i, rank, z, global.v[i]);
-      rabit::Allgather(all.data(), all.size(), rank * n, (rank + 1) * n, n);
+      rabit::Allgather(all.data(), all.size(), rank * n, n, n);  // begin, size, prev size
       for (int r = 0; r < world; ++r) {
         for (size_t i = 0; i < n; ++i) {
           rabit::utils::Check(all[r * n + i] == Contrib(i, r, z, global.v[i]),

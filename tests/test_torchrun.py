@@ -26,5 +26,9 @@ def test_torchrun_rendezvous(native_build, n):
                           "--master-port", str(port),
                           os.path.join(ROOT, "tests", "scripts", "torchrun_check.py")],
                          capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
-    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    if out.returncode != 0:
+        # the worker's own error lines first (torch.elastic's summary buries them)
+        keep = [l for l in (out.stdout + out.stderr).splitlines()
+                if "rabit" in l.lower() or "Error" in l or "error" in l][:40]
+        raise AssertionError("\n".join(keep) + "\n----\n" + out.stderr[-3000:])
     assert out.stdout.count("TORCHRUN OK") == n
