@@ -16,7 +16,9 @@
  *    store) are nontemporal: two inputs -> third buffer 71 -> 57 us per 128 MiB; nontemporal
  *    loads, and nontemporal stores for in-place / copy, measured neutral to 9 % slower.
  * MFMA is deliberately not used: an element-wise reduce has no data reuse; a ones-vector GEMM
- * over stacked peer buffers moves the same bytes and only adds matrix-pipe work.
+ * over stacked peer buffers moves the same bytes and only adds matrix-pipe work.  Measured
+ * (tools/mfma_reduce_probe.hip, profiles/r1_mfma_probe/): 8-source fp32 sum of 16 MiB segments,
+ * VALU 28.2 us vs v_mfma_f32_32x32x2_f32 33.1 us vs LDS-staged 48.2 us.
  */
 #include <hip/hip_runtime.h>
 
