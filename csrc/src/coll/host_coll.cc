@@ -5,6 +5,7 @@
 #include "coll/host_coll.h"
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 #include "rabit/internal/utils.h"
@@ -76,8 +77,13 @@ size_t DTypeSize(DataType dtype) {
   }
 }
 
-Status HostCollectives::Allreduce(void *buf, size_t tn, size_t count, ReduceFn red) {
-  if (count > cfg_->reduce_ring_mincount) return RingAllreduce(buf, tn, count, red);
+Status HostCollectives::Allreduce(void *buf, size_t tn, size_t count, ReduceFn red,
+                                  const void *src) {
+  if (count > cfg_->reduce_ring_mincount && *world_ > 1) {
+    return RingAllreduce(buf, tn, count, red, src);
+  }
+  // the tree path is latency-bound (small counts): stage the input
+  if (src != nullptr && src != buf) std::memcpy(buf, src, tn * count);
   return TreeAllreduce(buf, tn, count, red);
 }
 
@@ -182,12 +188,14 @@ Status HostCollectives::TreeAllreduce(void *buf_, size_t tn, size_t count, Reduc
 }
 
 namespace {
+constexpr size_t kOutOfPlacePiece = 256u << 10;
 inline size_t SegBegin(size_t k, size_t step, size_t count, size_t tn) {
   return std::min(k * step, count) * tn;
 }
 }  // namespace
 
-Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, ReduceFn red) {
+Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, ReduceFn red,
+                                          const void *src_) {
   const int n = *world_;
   if (n <= 1 || count == 0) return Status::kSuccess;
   PeerLink *next = topo_->ring_next, *prev = topo_->ring_prev;
@@ -196,6 +204,7 @@ Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, R
   utils::Assert(next->rank == (rank + 1) % n && prev->rank == (rank + n - 1) % n,
                 "ring must be relabelled so that next == rank + 1");
   char *buf = static_cast<char *>(buf_);
+  const char *src = src_ == buf_ ? nullptr : static_cast<const char *>(src_);
   const size_t total = tn * count;
   const size_t step = (count + n - 1) / n;
   const MPI::Datatype dt(tn);
@@ -210,6 +219,9 @@ Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, R
   const size_t stop_read = total + write_ptr;
   size_t stop_write = total + SegBegin(rank, step, count, tn);
   if (stop_write > stop_read) stop_write -= total;
+  // the first segment streamed out (the successor's) is raw input: out of place it is sent
+  // straight from src; everything after it is sent from buf once reduced
+  const size_t raw_end = read_ptr;
   next->InitRing(tn, step, cfg_->reduce_buffer_bytes);
   next->size_read = read_ptr;
   const size_t cap = next->ring_bytes();
@@ -236,16 +248,27 @@ Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, R
       while (reduce_ptr < max_reduce) {
         const size_t roff = reduce_ptr % cap;
         const size_t boff = reduce_ptr % total;
-        const size_t len = std::min({max_reduce - reduce_ptr, cap - roff, total - boff});
+        size_t len = std::min({max_reduce - reduce_ptr, cap - roff, total - boff});
+        if (src != nullptr) {
+          // buf = src op received, in cache-sized pieces (the copy's lines are still in cache
+          // when the reduction rewrites them)
+          len = std::min(len, std::max<size_t>(kOutOfPlacePiece / tn, 1) * tn);
+          std::memcpy(buf + boff, src + boff, len);
+        }
         red(next->ring() + roff, buf + boff, static_cast<int>(len / tn), dt);
         reduce_ptr += len;
       }
     }
     if (write_ptr < stop_write && write_ptr < reduce_ptr && poller.CanWrite(prev->sock.fd())) {
-      const size_t lim = std::min(reduce_ptr, stop_write);
+      size_t lim = std::min(reduce_ptr, stop_write);
+      const char *from = buf;
+      if (src != nullptr && write_ptr < raw_end) {
+        lim = std::min(lim, raw_end);
+        from = src;
+      }
       const size_t start = write_ptr % total;
       const size_t len = std::min(lim - write_ptr, total - start);
-      ssize_t k = prev->sock.Send(buf + start, len);
+      ssize_t k = prev->sock.Send(from + start, len);
       if (k >= 0) {
         write_ptr += static_cast<size_t>(k);
       } else {
@@ -257,8 +280,9 @@ Status HostCollectives::RingReduceScatter(void *buf_, size_t tn, size_t count, R
   return Status::kSuccess;
 }
 
-Status HostCollectives::RingAllreduce(void *buf, size_t tn, size_t count, ReduceFn red) {
-  Status s = RingReduceScatter(buf, tn, count, red);
+Status HostCollectives::RingAllreduce(void *buf, size_t tn, size_t count, ReduceFn red,
+                                      const void *src) {
+  Status s = RingReduceScatter(buf, tn, count, red, src);
   if (s != Status::kSuccess) return s;
   const int n = *world_;
   if (n <= 1) return Status::kSuccess;

@@ -46,11 +46,19 @@ class HostCollectives {
   /*! \brief link that caused the last error (reference err_link) */
   PeerLink *err_link() const { return err_link_; }
 
-  /*! \brief tree for small counts, ring (RS+AG) for large ones */
-  Status Allreduce(void *buf, size_t type_nbytes, size_t count, ReduceFn red);
+  /*!
+   * \brief tree for small counts, ring (RS+AG) for large ones.  src != nullptr: out of place,
+   *        the inputs are read from src and buf only receives results (src is never written,
+   *        so a failed attempt can be retried from it)
+   */
+  Status Allreduce(void *buf, size_t type_nbytes, size_t count, ReduceFn red,
+                   const void *src = nullptr);
   Status TreeAllreduce(void *buf, size_t type_nbytes, size_t count, ReduceFn red);
-  Status RingReduceScatter(void *buf, size_t type_nbytes, size_t count, ReduceFn red);
-  Status RingAllreduce(void *buf, size_t type_nbytes, size_t count, ReduceFn red);
+  /*! \brief after it, this rank's segment of buf is reduced (src: see Allreduce) */
+  Status RingReduceScatter(void *buf, size_t type_nbytes, size_t count, ReduceFn red,
+                           const void *src = nullptr);
+  Status RingAllreduce(void *buf, size_t type_nbytes, size_t count, ReduceFn red,
+                       const void *src = nullptr);
   Status RingAllgather(void *buf, size_t total, size_t slice_begin, size_t slice_end,
                        size_t size_prev_slice);
   Status TreeBroadcast(void *buf, size_t size, int root);

@@ -95,6 +95,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
+  if (is("rabit_host_out_of_place")) host_out_of_place_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
   if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
   if (is("rabit_trace_roctx")) trace_roctx_ = utils::StringToBool(val);
@@ -224,7 +225,7 @@ void EngineBase::ReportStatus() const {
   }
 }
 
-Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
+Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec, const void *src) {
   const size_t bytes = spec.bytes();
   if (host_via_device_ && dev_ && GetWorldSize() > 1 && spec.builtin() && bytes >= host_dev_min_ &&
       !(spec.op == mpi::kBitwiseOR && (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble))) {
@@ -233,7 +234,7 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
     void *d = dev_->Scratch(bytes, 2);
     Status s = EnsureDeviceComm();
     if (s != Status::kSuccess) return s;
-    dev_->StageToDevice(d, buf, bytes);
+    dev_->StageToDevice(d, src != nullptr ? src : buf, bytes);
     stats_.n_device_ops += 1;
     s = dev_->Allreduce(d, d, nullptr, spec.count, spec.dtype, spec.op, device::kPrepCopy, 1.0,
                         MakeProbe());
@@ -249,7 +250,7 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec) {
     if (fast != nullptr) red = fast;
   }
   utils::Check(red != nullptr, "Allreduce: no reducer for dtype %d op %d", spec.dtype, spec.op);
-  return host_->Allreduce(buf, spec.type_nbytes, spec.count, red);
+  return host_->Allreduce(buf, spec.type_nbytes, spec.count, red, src);
 }
 
 Status EngineBase::EnsureDeviceComm() {

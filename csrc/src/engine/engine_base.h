@@ -115,7 +115,9 @@ class EngineBase : public IEngine {
   };
   bool OnDevice(const void *p) const;
   /*! \brief in-place allreduce over the host plane */
-  Status TryAllreduceHost(void *buf, const ReduceSpec &spec);
+  /*! \brief host-buffer allreduce into buf; src != nullptr: inputs read from src (out of
+   *  place, src untouched, so a failed attempt can be retried) */
+  Status TryAllreduceHost(void *buf, const ReduceSpec &spec, const void *src = nullptr);
   /*!
    * \brief device allreduce dst = reduce(src) (src may equal dst); custom host reducers are
    *        staged through host memory
@@ -158,6 +160,9 @@ class EngineBase : public IEngine {
   bool timeout_enabled_{false};
   int timeout_sec_{1800};
   bool world1_fastpath_{true};
+  // robust engine, host buffers: reduce out of place from the user buffer into the result log
+  // (one copy per op instead of two)
+  bool host_out_of_place_{true};
   bool calibrate_{true};
   bool calibrate_test_{false};  // run the calibration without RCCL (tests on a shared GPU)
   bool device_replay_{true};       // recover HBM results with a device broadcast

@@ -5,6 +5,8 @@
  */
 #include "engine/engine_robust.h"
 
+#include <sys/mman.h>
+
 #include <unistd.h>
 
 #include <algorithm>
@@ -39,9 +41,14 @@ void *EngineRobust::ResultLog::HostArena::Alloc(size_t bytes) {
     ++cur_;
   }
   Chunk c;
-  c.size = std::max<size_t>(need, 64u << 20);
-  c.base = static_cast<char *>(std::aligned_alloc(64, (c.size + 63) & ~static_cast<size_t>(63)));
+  // 2 MiB aligned and backed by transparent huge pages where the kernel allows it: a result
+  // log chunk is written once per op in full, and 4 KiB first-touch faults on fresh chunks
+  // cost as much as the copy itself
+  constexpr size_t kHuge = 2u << 20;
+  c.size = (std::max<size_t>(need, 64u << 20) + kHuge - 1) & ~(kHuge - 1);
+  c.base = static_cast<char *>(std::aligned_alloc(kHuge, c.size));
   utils::Check(c.base != nullptr, "out of host memory for the result log (%zu bytes)", c.size);
+  (void)madvise(c.base, c.size, MADV_HUGEPAGE);
   c.used = need;
   chunks_.push_back(c);
   cur_ = chunks_.size() - 1;
@@ -310,8 +317,13 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
       s = TryAllreduceDevice(prep_src != nullptr ? prep_src : buf, temp, spec, buf,
                              prep_src != nullptr ? prep_op : device::kPrepCopy, prep_alpha);
     } else {
-      std::memcpy(temp, buf, bytes);
-      s = TryAllreduceHost(temp, spec);
+      // out of place: the log slot receives the result, buf keeps the input until success
+      if (host_out_of_place_) {
+        s = TryAllreduceHost(temp, spec, buf);
+      } else {
+        std::memcpy(temp, buf, bytes);
+        s = TryAllreduceHost(temp, spec);
+      }
     }
     if (CheckAndRecover(s)) {
       if (!dev) std::memcpy(buf, temp, bytes);

@@ -13,6 +13,8 @@ Appendix A) for each world size, then prints one JSON line per (implementation, 
 Implementations:
   reference  - the reference robust engine, host buffers over TCP (its only data path)
   xrabit     - xrabit's robust engine, host buffers over TCP (the same job on our host plane)
+  xrabit_inplace - xrabit's robust engine copying the input into the result log first
+               (rabit_host_out_of_place=0, the reference's scheme) for A/B runs
   xrabit_dev - xrabit with HBM buffers (device=1); only at world 1 unless --dev-worlds is
                given (several ranks on one GPU share its HBM: not an xGMI number)
 """
@@ -74,6 +76,8 @@ def main():
                 continue
             cmd = {"reference": [ref, str(args.n), str(args.nrep)],
                    "xrabit": [ours, str(args.n), str(args.nrep)],
+                   "xrabit_inplace": [ours, str(args.n), str(args.nrep),
+                                      "rabit_host_out_of_place=0"],
                    "xrabit_dev": [ours, str(args.n), str(args.nrep), "device=1",
                                   "rabit_world1_fastpath=0"]}[impl]
             port += 7
