@@ -1,7 +1,9 @@
 """Initialise rabit inside a `torch.distributed.run` (torchrun) job.
 
 torchrun gives every process RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT but
-no rabit tracker.  Rank 0 hosts the tracker in a background thread at MASTER_PORT + offset;
+no rabit tracker.  Rank 0 hosts the tracker in a background thread on a free port from
+MASTER_PORT + offset on and publishes it in torchrun's agent store (outside torchrun: exactly
+MASTER_PORT + offset);
 every rank joins with its torchrun RANK as task id, so the tracker's batch assignment (ordered
 by host, then numeric task id) gives rabit rank == torchrun RANK on a single node, and the
 device plane picks the GPU from LOCAL_RANK (one process per GPU, RCCL over xGMI).
@@ -27,6 +29,20 @@ class TorchrunContext:
             self.tracker.join(timeout)
 
 
+def _agent_store(addr: str, port: int):
+    """a client of the TCPStore torchrun's agent serves at MASTER_ADDR:MASTER_PORT (the store
+    torch.distributed's env:// rendezvous uses under torchrun), or None outside torchrun"""
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() != "true":
+        return None
+    try:
+        from datetime import timedelta
+
+        from torch.distributed import TCPStore
+        return TCPStore(addr, port, is_master=False, timeout=timedelta(seconds=300))
+    except Exception:  # noqa: BLE001 - fall back to the fixed port offset
+        return None
+
+
 def init_from_env(lib: str = "standard", port_offset: int = TRACKER_PORT_OFFSET,
                   **params) -> TorchrunContext:
     rank = int(os.environ.get("RANK", "0"))
@@ -41,11 +57,24 @@ def init_from_env(lib: str = "standard", port_offset: int = TRACKER_PORT_OFFSET,
         tracker.start(1)
         port = tracker.port
     else:
-        port = master_port + port_offset
-        if rank == 0:
-            tracker = RabitTracker(addr, world, port=port, port_end=port + 1,
-                                   print_fn=lambda m: None)
-            tracker.start(world)
+        store = _agent_store(addr, master_port)
+        if store is not None:
+            # torchrun's own store carries the tracker port: rank 0 binds any free port near
+            # MASTER_PORT + offset and publishes it (keyed by the restart round)
+            key = "xrabit/tracker_port/%s" % os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+            if rank == 0:
+                start = master_port + port_offset
+                tracker = RabitTracker(addr, world, port=start, port_end=start + 200,
+                                       print_fn=lambda m: None)
+                tracker.start(world)
+                store.set(key, str(tracker.port))
+            port = int(store.get(key).decode())
+        else:
+            port = master_port + port_offset
+            if rank == 0:
+                tracker = RabitTracker(addr, world, port=port, port_end=port + 1,
+                                       print_fn=lambda m: None)
+                tracker.start(world)
     args = dict(rabit_tracker_uri=addr, rabit_tracker_port=port, rabit_task_id=rank,
                 rabit_world_size=world, DMLC_WORKER_CONNECT_RETRY=30)
     if "rabit_device" not in params:
