@@ -29,6 +29,14 @@ class TorchrunContext:
             self.tracker.join(timeout)
 
 
+def _node_has_gpus() -> bool:
+    try:
+        import torch
+        return torch.cuda.device_count() > 0  # counts devices without initialising HIP
+    except Exception:  # noqa: BLE001
+        return False
+
+
 def _agent_store(addr: str, port: int):
     """a client of the TCPStore torchrun's agent serves at MASTER_ADDR:MASTER_PORT (the store
     torch.distributed's env:// rendezvous uses under torchrun), or None outside torchrun"""
@@ -79,6 +87,10 @@ def init_from_env(lib: str = "standard", port_offset: int = TRACKER_PORT_OFFSET,
                 rabit_world_size=world, DMLC_WORKER_CONNECT_RETRY=30)
     if "rabit_device" not in params:
         params["rabit_device"] = local_rank
+    if "rabit_host_via_device" not in params and _node_has_gpus():
+        # one process per GPU: every rank has a device plane, so large host-buffer allreduces
+        # can uniformly take the HBM transports (staged over PCIe) instead of loopback TCP
+        params["rabit_host_via_device"] = 1
     args.update(params)
     rabit.init(lib=lib, **args)
     assert rabit.get_world_size() == world, "rabit world size differs from torchrun's"

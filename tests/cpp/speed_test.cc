@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -55,7 +56,10 @@ int main(int argc, char *argv[]) {
   rabit::Init(argc, argv);
   const int rank = rabit::GetRank();
   const int world = rabit::GetWorldSize();
-  srand(0);
+  // broadcast roots from a generator of our own: the reference draws them with rand(), whose
+  // global state the GPU runtime may advance by different amounts on different ranks (seen with
+  // HBM staging: ranks disagreed on the root and the job desynchronised)
+  std::mt19937 roots(0);
   std::vector<float> host(n);
   std::string bstr(n, '\0');
   float *fbuf = host.data();
@@ -82,7 +86,7 @@ int main(int argc, char *argv[]) {
     if (on_device) (void)hipDeviceSynchronize();
     g_sum += rabit::utils::GetTime() - t;
 
-    const int root = rand() % world;
+    const int root = static_cast<int>(roots() % static_cast<unsigned>(world));
     t = rabit::utils::GetTime();
     rabit::Broadcast(bbuf, n, root);
     if (on_device) (void)hipDeviceSynchronize();

@@ -15,6 +15,8 @@ Implementations:
   xrabit     - xrabit's robust engine, host buffers over TCP (the same job on our host plane)
   xrabit_inplace - xrabit's robust engine copying the input into the result log first
                (rabit_host_out_of_place=0, the reference's scheme) for A/B runs
+  xrabit_via_dev - host buffers staged through HBM onto the device transports
+               (rabit_host_via_device=1; the MPI-engine role on a GPU node)
   xrabit_dev - xrabit with HBM buffers (device=1); only at world 1 unless --dev-worlds is
                given (several ranks on one GPU share its HBM: not an xGMI number)
 """
@@ -78,6 +80,8 @@ def main():
                    "xrabit": [ours, str(args.n), str(args.nrep)],
                    "xrabit_inplace": [ours, str(args.n), str(args.nrep),
                                       "rabit_host_out_of_place=0"],
+                   "xrabit_via_dev": [ours, str(args.n), str(args.nrep),
+                                      "rabit_host_via_device=1"],
                    "xrabit_dev": [ours, str(args.n), str(args.nrep), "device=1",
                                   "rabit_world1_fastpath=0"]}[impl]
             port += 7
