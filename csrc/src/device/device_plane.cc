@@ -474,10 +474,6 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
   (void)probe;
   utils::Check(comm_ != nullptr, "device allreduce without communicator");
   const int n = nranks_;
-  if (n == 1) {
-    CopyDeviceAsync(recv, send, count * tn);
-    return Status::kSuccess;
-  }
   // all-to-all: rank k receives everyone's copy of segment k, reduces it with the
   // multi-source kernel, then an allgather distributes the reduced segments
   const size_t seg = (count + n - 1) / n;

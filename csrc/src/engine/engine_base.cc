@@ -96,6 +96,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_host_out_of_place")) host_out_of_place_ = utils::StringToBool(val);
+  if (is("rabit_device_world1_transport")) world1_transport_ = utils::StringToBool(val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
   if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
   if (is("rabit_trace_roctx")) trace_roctx_ = utils::StringToBool(val);
@@ -430,7 +431,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     utils::Check(prep == device::kPrepCopy, "fused prepare needs a built-in reduction");
     stats_.n_device_ops += 1;
     trace::Scope ts("device_allreduce", rank_, version_number_, seq_counter_, bytes, 1);
-    if (GetWorldSize() == 1) {
+    if (GetWorldSize() == 1 && !world1_transport_) {
       dev_->CopyDeviceAsync(dst, src, bytes);
       if (dst2 != nullptr && dst2 != src) dev_->CopyDeviceAsync(dst2, src, bytes);
       return dev_->Finish(MakeProbe(), false);  // no peer can fail: stream-ordered, no host wait
@@ -455,7 +456,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   }
   stats_.n_device_ops += 1;
   trace::Scope ts("device_allreduce", rank_, version_number_, seq_counter_, bytes, 1);
-  if (GetWorldSize() == 1) {
+  if (GetWorldSize() == 1 && !world1_transport_) {
     // a one-rank reduction is the identity: only materialise it where it was asked for
     if (prep != device::kPrepCopy) {
       device::CheckHip(device::LaunchPrepare(dst, dst2, src, spec.count, spec.dtype, prep, alpha,
@@ -477,8 +478,11 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
 }
 
 Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
-  if (size == 0 || GetWorldSize() == 1) return Status::kSuccess;
-  if (!OnDevice(buf)) return host_->TreeBroadcast(buf, size, root);
+  if (size == 0) return Status::kSuccess;
+  if (!OnDevice(buf)) {
+    return GetWorldSize() == 1 ? Status::kSuccess : host_->TreeBroadcast(buf, size, root);
+  }
+  if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
@@ -490,8 +494,12 @@ Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
 
 Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t end,
                                 size_t prev_size) {
-  if (total == 0 || GetWorldSize() == 1) return Status::kSuccess;
-  if (!OnDevice(buf)) return host_->RingAllgather(buf, total, begin, end, prev_size);
+  if (total == 0) return Status::kSuccess;
+  if (!OnDevice(buf)) {
+    return GetWorldSize() == 1 ? Status::kSuccess
+                               : host_->RingAllgather(buf, total, begin, end, prev_size);
+  }
+  if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   // every rank needs every slice: exchange (begin, size) pairs over the host ring first
   const int n = GetWorldSize();
   std::vector<uint64_t> meta(2 * n, 0);

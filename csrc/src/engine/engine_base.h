@@ -163,6 +163,9 @@ class EngineBase : public IEngine {
   // robust engine, host buffers: reduce out of place from the user buffer into the result log
   // (one copy per op instead of two)
   bool host_out_of_place_{true};
+  // test hook: world-1 device ops go through the transports (a one-rank RCCL communicator, a
+  // one-peer direct group) instead of the local short-cut, so their API paths run on one GPU
+  bool world1_transport_{false};
   bool calibrate_{true};
   bool calibrate_test_{false};  // run the calibration without RCCL (tests on a shared GPU)
   bool device_replay_{true};       // recover HBM results with a device broadcast

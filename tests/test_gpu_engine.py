@@ -1,8 +1,9 @@
 """Device data plane through the engine on one MI355X (world size 1, full robust path).
 
-Multi-GPU RCCL paths cannot run on the 1-GPU box (RCCL refuses two ranks on one GPU); the
-multi-rank control flow they share is covered by the CPU tests, and the driver's 8-GPU bench
-exercises the RCCL ring.
+Multi-GPU RCCL paths cannot run on the 1-GPU box (RCCL refuses two ranks on one GPU); their
+API calls run here through a one-rank communicator (test_transports_world1), the multi-rank
+control flow is covered by the CPU tests and the shared-GPU direct-transport tests, and the
+driver's 8-GPU bench exercises RCCL with 8 ranks.
 """
 import os
 import subprocess
@@ -113,3 +114,16 @@ def test_bench_n1(tmp_path):
     assert len(lines) == 1
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 1 and rec["value"] > 0
+
+
+@pytest.mark.parametrize("algo", ["rccl", "direct", "auto"])
+def test_transports_world1(algo):
+    """RCCL and direct-transport API paths on the box's one GPU (a one-rank communicator /
+    group): the 8-GPU runs use the same calls with more ranks."""
+    from rabit_amd.launcher import LocalJob
+    job = LocalJob([sys.executable, os.path.join(ROOT, "tests", "scripts", "transport_world1.py"),
+                    algo], 1, 1, capture=True, timeout=240, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-5000:]
+    assert "TRANSPORT1 OK" in out, out[-3000:]
