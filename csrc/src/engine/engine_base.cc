@@ -97,6 +97,9 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_host_out_of_place")) host_out_of_place_ = utils::StringToBool(val);
   if (is("rabit_device_world1_transport")) world1_transport_ = utils::StringToBool(val);
+  if (is("rabit_host_shm")) shm_enabled_ = utils::StringToBool(val);
+  if (is("rabit_host_shm_min")) shm_min_ = core::ParseUnit(name, val);
+  if (is("rabit_host_shm_buffer")) shm_stage_ = core::ParseUnit(name, val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
   if (is("rabit_trace")) trace_spans_ = utils::StringToBool(val);
   if (is("rabit_trace_roctx")) trace_roctx_ = utils::StringToBool(val);
@@ -154,6 +157,7 @@ bool EngineBase::Init(int argc, char *argv[]) {
 
 bool EngineBase::Shutdown() {
   try {
+    ResetShm();
     if (dev_) {
       dev_->Synchronize();
       dev_ckpt_.reset();
@@ -251,7 +255,43 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec, const voi
     if (fast != nullptr) red = fast;
   }
   utils::Check(red != nullptr, "Allreduce: no reducer for dtype %d op %d", spec.dtype, spec.op);
+  if (UseShm(bytes)) {
+    Status s = EnsureShm();
+    if (s != Status::kSuccess) return s;
+    if (shm_ != nullptr) {
+      stats_.n_shm_ops += 1;
+      return shm_->Allreduce(src != nullptr ? src : buf, buf, spec.type_nbytes, spec.count, red,
+                             MakeProbe());
+    }
+  }
   return host_->Allreduce(buf, spec.type_nbytes, spec.count, red, src);
+}
+
+Status EngineBase::EnsureShm() {
+  if (shm_decided_) return Status::kSuccess;
+  const int n = GetWorldSize();
+  std::unique_ptr<coll::ShmGroup> g(
+      new coll::ShmGroup(shm_stage_, timeout_enabled_ ? timeout_sec_ : 1800.0));
+  const size_t rb = sizeof(coll::ShmRecord);
+  std::vector<coll::ShmRecord> all(n);
+  std::memset(all.data(), 0, rb * n);
+  all[rank_] = g->local();
+  Status s = host_->RingAllgather(all.data(), rb * n, rb * rank_, rb * (rank_ + 1), rb);
+  if (s != Status::kSuccess) return s;
+  std::string why;
+  int ok = n <= coll::kMaxShmRanks && g->ok() && g->Open(all, rank_, &why) ? 1 : 0;
+  s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  if (ok) {
+    s = g->Seal(MakeProbe());
+    if (s != Status::kSuccess) return s;
+    shm_ = std::move(g);
+  } else if (debug_) {
+    utils::HandleLogInfo("[%d] shared-memory transport off for this epoch%s%s\n", rank_,
+                         why.empty() ? "" : ": ", why.c_str());
+  }
+  shm_decided_ = true;
+  return Status::kSuccess;
 }
 
 Status EngineBase::EnsureDeviceComm() {
@@ -480,7 +520,16 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
 Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
   if (size == 0) return Status::kSuccess;
   if (!OnDevice(buf)) {
-    return GetWorldSize() == 1 ? Status::kSuccess : host_->TreeBroadcast(buf, size, root);
+    if (GetWorldSize() == 1) return Status::kSuccess;
+    if (UseShm(size)) {
+      Status s = EnsureShm();
+      if (s != Status::kSuccess) return s;
+      if (shm_ != nullptr) {
+        stats_.n_shm_ops += 1;
+        return shm_->Broadcast(buf, size, root, MakeProbe());
+      }
+    }
+    return host_->TreeBroadcast(buf, size, root);
   }
   if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   Status s = EnsureDeviceComm();
@@ -678,7 +727,7 @@ std::string EngineBase::StatsJson() const {
   }
   os << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
      << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
-     << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
+     << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_shm_ops\":" << s.n_shm_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
      << ",\"n_device_replays\":" << s.n_device_replays

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "coll/host_coll.h"
+#include "coll/shm_coll.h"
 #include "device/device_checkpoint.h"
 #include "device/device_plane.h"
 #include "net/links.h"
@@ -32,6 +33,7 @@ typedef IEngine::ReduceFunction *ReduceFn;
 struct EngineStats {
   uint64_t n_allreduce{0}, n_broadcast{0}, n_allgather{0}, n_checkpoint{0};
   uint64_t n_device_ops{0}, n_recovered_ops{0}, n_recover_events{0}, n_consensus{0};
+  uint64_t n_shm_ops{0};
   uint64_t n_consensus_elided{0};
   uint64_t n_device_replays{0};
   uint64_t n_device_ckpt_loads{0};  // checkpoint loads served by device broadcasts  // results recovered by a device broadcast (one xGMI hop)
@@ -133,6 +135,16 @@ class EngineBase : public IEngine {
   /*! \brief build the device transports if missing (collective): exchange GPU records, map
    *  the peers' buffers for the direct transport, build the RCCL communicator */
   Status EnsureDeviceComm();
+  /*! \brief true if a host-buffer op of this size goes through shared memory */
+  bool UseShm(size_t bytes) const { return shm_enabled_ && world_size_ > 1 && bytes >= shm_min_; }
+  /*! \brief build the shared-memory group (collective; uniform outcome: usable on every rank
+   *  or off for this epoch) */
+  Status EnsureShm();
+  /*! \brief forget the group (after a failure every rank rebuilds it) */
+  void ResetShm() {
+    shm_.reset();
+    shm_decided_ = false;
+  }
   /*! \brief auto mode: time RCCL and the direct transport at two sizes, verify the direct
    *  result, and set the size from which ops go direct (collective) */
   Status CalibrateDevice();
@@ -166,6 +178,9 @@ class EngineBase : public IEngine {
   // test hook: world-1 device ops go through the transports (a one-rank RCCL communicator, a
   // one-peer direct group) instead of the local short-cut, so their API paths run on one GPU
   bool world1_transport_{false};
+  bool shm_enabled_{true};          // rabit_host_shm
+  size_t shm_min_{1u << 20};        // rabit_host_shm_min
+  size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)
   bool calibrate_{true};
   bool calibrate_test_{false};  // run the calibration without RCCL (tests on a shared GPU)
   bool device_replay_{true};       // recover HBM results with a device broadcast
@@ -181,6 +196,10 @@ class EngineBase : public IEngine {
   // runtime state
   net::Topology topo_;
   std::unique_ptr<coll::HostCollectives> host_;
+  /*! \brief shared-memory transport for large host buffers of co-located ranks (built on
+   *  first use after every (re)connect, like a device epoch; nullptr while undecided or off) */
+  std::unique_ptr<coll::ShmGroup> shm_;
+  bool shm_decided_{false};
   std::unique_ptr<device::DevicePlane> dev_;
   std::unique_ptr<device::DeviceCheckpoint> dev_ckpt_;
   void *user_stream_{nullptr};

@@ -193,6 +193,7 @@ void EngineRobust::InitAfterException() {
   // drop every link and rejoin through the tracker, as after a failure
   for (auto &l : topo_.links) l->sock.Close();
   if (dev_) dev_->AbortComm();
+  ResetShm();
   fast_mode_ = false;
   ReconnectLinks("recover");
 }

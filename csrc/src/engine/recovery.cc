@@ -50,6 +50,8 @@ bool EngineRobust::CheckAndRecover(Status s) {
   }
   // the communicator contains the failed peer: abort it, a new epoch is built on demand
   if (dev_) dev_->AbortComm();
+  // the shared-memory group contains the failed peer too: rebuilt on first use after rejoin
+  ResetShm();
   // simplest consistent repair: drop every link so the failure propagates, then rejoin
   for (auto &l : topo_.links) l->sock.Close();
   // spread the reconnect load on the tracker

@@ -11,6 +11,7 @@
  * With rabit_bootstrap_cache=1 a bootstrap Allreduce<Max> runs before LoadCheckPoint.
  * Usage: recover_test <ndata> mode=<global|local|lazy> [niter=3] [rabit params...]
  */
+#include <rabit/c_api.h>
 #include <rabit/rabit.h>
 
 #include <cmath>
@@ -144,7 +145,11 @@ int main(int argc, char *argv[]) {
     printf("[%d] iteration %d done (version %d)\n", rank, it, rabit::VersionNumber());
     fflush(stdout);
   }
+  // transports used (extension of the C API): {"n_shm_ops":...} etc.
+  const std::string stats = RabitGetStats();
+  const size_t at = stats.find("\"n_shm_ops\":");
+  const long shm_ops = at == std::string::npos ? -1 : atol(stats.c_str() + at + 12);
   rabit::Finalize();
-  printf("[%d] PASSED\n", rank);
+  printf("[%d] PASSED shm_ops=%ld\n", rank, shm_ops);
   return 0;
 }

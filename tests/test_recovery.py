@@ -73,3 +73,17 @@ def test_lazy_prepare_not_rerun_on_replay(native_build):
     assert out.count("DONE") == 4
     # rank 1 died at seq 1 of version 0 and replayed seq 0 without preparing it again
     assert "[1] replayed-prepare-skipped" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("mode,kills", [("global", DIE_HARD), ("local", LOCAL), ("lazy", DIE_SAME)])
+def test_recover_shared_memory_transport(native_build, mode, kills):
+    """Large host ops take the shared-memory transport between co-located ranks; kills in the
+    middle of the job force the group to be rebuilt after every recovery (and a restarted
+    worker to join a new one) while the replay protocol serves the missed results."""
+    args = ["mode=" + mode, "rabit_host_shm_min=64K", "rabit_host_shm_buffer=1M"] + kills
+    rc, job, out = _run([os.path.join(native_build, "recover_test"), "70000"] + args, n=6)
+    assert rc == 0, out[-4000:]
+    assert out.count("PASSED") == 6, out[-4000:]
+    assert sum(a - 1 for a in job.attempts) >= 2
+    import re
+    assert all(int(k) > 0 for k in re.findall(r"PASSED shm_ops=(-?\d+)", out)), out[-2000:]

@@ -12,7 +12,9 @@ Appendix A) for each world size, then prints one JSON line per (implementation, 
 
 Implementations:
   reference  - the reference robust engine, host buffers over TCP (its only data path)
-  xrabit     - xrabit's robust engine, host buffers over TCP (the same job on our host plane)
+  xrabit     - xrabit's robust engine, host buffers (shared memory between co-located ranks
+               for large ops, TCP otherwise)
+  xrabit_tcp - xrabit's host path over loopback TCP only (rabit_host_shm=0)
   xrabit_inplace - xrabit's robust engine copying the input into the result log first
                (rabit_host_out_of_place=0, the reference's scheme) for A/B runs
   xrabit_via_dev - host buffers staged through HBM onto the device transports
@@ -78,6 +80,7 @@ def main():
                 continue
             cmd = {"reference": [ref, str(args.n), str(args.nrep)],
                    "xrabit": [ours, str(args.n), str(args.nrep)],
+                   "xrabit_tcp": [ours, str(args.n), str(args.nrep), "rabit_host_shm=0"],
                    "xrabit_inplace": [ours, str(args.n), str(args.nrep),
                                       "rabit_host_out_of_place=0"],
                    "xrabit_via_dev": [ours, str(args.n), str(args.nrep),
