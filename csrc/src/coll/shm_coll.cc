@@ -208,5 +208,45 @@ Status ShmGroup::Broadcast(void *buf_, size_t bytes, int root, const Probe &prob
   ++ops_;
   return Status::kSuccess;
 }
+
+Status ShmGroup::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
+                            const std::vector<size_t> &size, const Probe &probe) {
+  char *buf = static_cast<char *>(buf_);
+  // the (at most two) byte ranges of slice r in [0, total)
+  auto ranges = [&](int r, size_t lo[2], size_t hi[2]) {
+    if (size[r] == 0) return 0;
+    const size_t b = begin[r] % total;
+    lo[0] = b;
+    hi[0] = std::min(total, b + size[r]);
+    if (b + size[r] <= total) return 1;
+    lo[1] = 0;
+    hi[1] = b + size[r] - total;
+    return 2;
+  };
+  // windows of one stage buffer each; a window holds the bytes [wlo, whi) of buf
+  for (size_t wlo = 0; wlo < total; wlo += stage_bytes_) {
+    const size_t whi = std::min(total, wlo + stage_bytes_);
+    const int which = parity_;
+    parity_ ^= 1;
+    size_t lo[2], hi[2];
+    int k = ranges(rank_, lo, hi);
+    for (int j = 0; j < k; ++j) {
+      const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
+      if (z > a) std::memcpy(stage(rank_, which) + (a - wlo), buf + a, z - a);
+    }
+    Status s = Barrier(probe);
+    if (s != Status::kSuccess) return s;
+    for (int p = 0; p < n_; ++p) {
+      if (p == rank_) continue;
+      k = ranges(p, lo, hi);
+      for (int j = 0; j < k; ++j) {
+        const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
+        if (z > a) std::memcpy(buf + a, stage(p, which) + (a - wlo), z - a);
+      }
+    }
+  }
+  ++ops_;
+  return Status::kSuccess;
+}
 }  // namespace coll
 }  // namespace rabit

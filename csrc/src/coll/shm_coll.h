@@ -12,6 +12,7 @@
  *    Each byte is copied once into shared memory and read where it is needed — over loopback
  *    TCP the reference moves every byte through two kernel copies per hop.
  *  - Broadcast: the root stages; barrier; everyone copies.
+ *  - AllgatherV (rabit's variable, wrapping slices): stage own slice; barrier; copy the rest.
  *
  * Stage buffers alternate between ops (parity), which lets two barriers per allreduce chunk
  * and one per broadcast chunk suffice.  The TCP links stay the control plane: a barrier gives
@@ -65,6 +66,12 @@ class ShmGroup {
   Status Allreduce(const void *src, void *dst, size_t tn, size_t count, ReduceFn red,
                    const Probe &probe);
   Status Broadcast(void *buf, size_t bytes, int root, const Probe &probe);
+  /*!
+   * \brief rabit's allgather with variable, wrapping slices: rank r owns bytes
+   *        [begin[r], begin[r] + size[r]) mod total of buf (every rank passes all slices)
+   */
+  Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
+                    const std::vector<size_t> &size, const Probe &probe);
   uint64_t ops() const { return ops_; }
 
  private:

@@ -545,8 +545,28 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
                                 size_t prev_size) {
   if (total == 0) return Status::kSuccess;
   if (!OnDevice(buf)) {
-    return GetWorldSize() == 1 ? Status::kSuccess
-                               : host_->RingAllgather(buf, total, begin, end, prev_size);
+    if (GetWorldSize() == 1) return Status::kSuccess;
+    if (UseShm(total)) {
+      Status s = EnsureShm();
+      if (s != Status::kSuccess) return s;
+      if (shm_ != nullptr) {
+        // every rank needs every slice: exchange (begin, size) pairs over the host ring first
+        const int n = GetWorldSize();
+        std::vector<uint64_t> meta(2 * n, 0);
+        meta[2 * rank_] = begin;
+        meta[2 * rank_ + 1] = end - begin;
+        s = host_->RingAllgather(meta.data(), meta.size() * 8, 16 * rank_, 16 * rank_ + 16, 16);
+        if (s != Status::kSuccess) return s;
+        std::vector<size_t> b(n), z(n);
+        for (int r = 0; r < n; ++r) {
+          b[r] = static_cast<size_t>(meta[2 * r]);
+          z[r] = static_cast<size_t>(meta[2 * r + 1]);
+        }
+        stats_.n_shm_ops += 1;
+        return shm_->AllgatherV(buf, total, b, z, MakeProbe());
+      }
+    }
+    return host_->RingAllgather(buf, total, begin, end, prev_size);
   }
   if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   // every rank needs every slice: exchange (begin, size) pairs over the host ring first
