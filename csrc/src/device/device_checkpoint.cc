@@ -15,10 +15,10 @@ namespace device {
 
 DeviceCheckpoint::DeviceCheckpoint(DevicePlane *plane) : plane_(plane) {
   CheckHip(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(ckpt)");
-  CheckHip(hipEventCreateWithFlags(&snap_done_, hipEventDisableTiming), "hipEventCreate");
   for (auto &h : half_) {
     h.owner = this;
     CheckHip(hipEventCreateWithFlags(&h.d2h_done, hipEventDisableTiming), "hipEventCreate");
+    CheckHip(hipEventCreateWithFlags(&h.snap_done, hipEventDisableTiming), "hipEventCreate");
   }
   loader_.owner = this;
 }
@@ -29,8 +29,8 @@ DeviceCheckpoint::~DeviceCheckpoint() {
     for (void *p : h.dev) (void)hipFree(p);
     if (h.pinned != nullptr) (void)hipHostFree(h.pinned);
     (void)hipEventDestroy(h.d2h_done);
+    (void)hipEventDestroy(h.snap_done);
   }
-  (void)hipEventDestroy(snap_done_);
   (void)hipStreamDestroy(side_);
 }
 
@@ -44,9 +44,10 @@ size_t DeviceCheckpoint::reserved_bytes() const {
 
 const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const size_t *nbytes,
                                                const std::string &meta) {
-  cur_ = 1 - cur_;
+  // the oldest slot: the newest two versions stay intact
+  cur_ = (cur_ + 1) % kSlots;
   Half &h = half_[cur_];
-  // the previous D2H of this half must be done before its buffers are reused
+  // a mirror still reading this slot must finish before its buffers are reused
   CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
   h.dev.resize(n, nullptr);
   h.cap.resize(n, 0);
@@ -70,24 +71,43 @@ const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const s
   // 1. HBM snapshot on the plane stream, ordered after the caller's stream
   plane_->EnterFromUser();
   for (int i = 0; i < n; ++i) plane_->CopyDeviceAsync(h.dev[i], ptrs[i], nbytes[i]);
-  CheckHip(hipEventRecord(snap_done_, plane_->stream()), "hipEventRecord(snapshot)");
+  CheckHip(hipEventRecord(h.snap_done, plane_->stream()), "hipEventRecord(snapshot)");
   // the caller may overwrite its tensors only after the snapshot read them
   plane_->Finish(FailureProbe(), false);
-  // 2. pinned host mirror on the side stream
-  CheckHip(hipStreamWaitEvent(side_, snap_done_, 0), "hipStreamWaitEvent(mirror)");
-  size_t off = 0;
-  for (int i = 0; i < n; ++i) {
-    if (nbytes[i] != 0) {
-      CheckHip(hipMemcpyAsync(h.pinned + off, h.dev[i], nbytes[i], hipMemcpyDeviceToHost, side_),
-               "D2H mirror");
-    }
-    off += nbytes[i];
+  // 2. pinned host mirror on the side stream: always, or when the previous one is done
+  h.mirror_valid = false;
+  bool idle = last_mirror_ == nullptr;
+  if (!idle) {
+    const hipError_t q = hipEventQuery(last_mirror_->d2h_done);
+    if (q != hipErrorNotReady) CheckHip(q, "checkpoint mirror query");
+    idle = q == hipSuccess;
   }
-  CheckHip(hipEventRecord(h.d2h_done, side_), "hipEventRecord(mirror)");
+  if (mirror_always_ || idle) {
+    h.StartMirror();
+    mirrors_ += 1;
+  } else {
+    mirrors_deferred_ += 1;  // copied on demand by Save if a peer asks for these bytes
+  }
   return &h;
 }
 
+void DeviceCheckpoint::Half::StartMirror() const {
+  CheckHip(hipStreamWaitEvent(owner->side_, snap_done, 0), "hipStreamWaitEvent(mirror)");
+  size_t off = 0;
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    if (sizes[i] != 0) {
+      CheckHip(hipMemcpyAsync(pinned + off, dev[i], sizes[i], hipMemcpyDeviceToHost, owner->side_),
+               "D2H mirror");
+    }
+    off += sizes[i];
+  }
+  CheckHip(hipEventRecord(d2h_done, owner->side_), "hipEventRecord(mirror)");
+  mirror_valid = true;
+  owner->last_mirror_ = this;
+}
+
 void DeviceCheckpoint::Half::Save(Stream *fo) const {
+  if (!mirror_valid) StartMirror();  // deferred mirror: a peer needs the bytes now
   CheckHip(hipEventSynchronize(d2h_done), "checkpoint mirror wait");
   uint64_t ml = meta.size();
   fo->Write(&ml, sizeof(ml));

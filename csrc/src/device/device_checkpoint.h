@@ -5,11 +5,16 @@
  * The reference serialises the global model into a host string at every CheckPoint.  For
  * device tensors that means a synchronous D2H of the whole model on the critical path.  Here
  * a checkpoint is:
- *   1. an HBM-to-HBM snapshot of the tensors (gfx950 copy kernel, ~6 TB/s) into one of two
- *      snapshot halves (double buffered: the previous version must stay intact until the new
- *      checkpoint is acknowledged, peers may still be loading it),
+ *   1. an HBM-to-HBM snapshot of the tensors (gfx950 copy kernel, ~6 TB/s) into the oldest of
+ *      kSlots snapshot slots (the previous version must stay intact until the new checkpoint
+ *      is acknowledged, peers may still be loading it; a third slot lets a host mirror still
+ *      be in flight),
  *   2. an asynchronous D2H copy of the snapshot into pinned host memory on a side stream
- *      (overlaps the next iteration; host-DRAM durability),
+ *      (overlaps the next iterations; host-DRAM durability).  In the default "idle" mode a
+ *      mirror starts only when the previous one has finished, so iterations shorter than a
+ *      PCIe copy of the model are never throttled by it; a snapshot that was not mirrored is
+ *      copied on demand if a peer asks for its bytes.  "always" mirrors every checkpoint
+ *      (rabit_device_ckpt_mirror=always),
  *   3. registration with the robust engine as a *lazy* checkpoint: bytes are produced (from the
  *      pinned mirror, after its event) only if a recovering peer requests them.
  * Wire format of the global checkpoint: uint64 meta_len, meta, uint64 n, n x uint64 size,
@@ -46,8 +51,18 @@ class DeviceCheckpoint {
   const std::string &loaded_meta() const { return loaded_meta_; }
 
   // ---- device-side recovery (the robust engine broadcasts snapshot buffers over xGMI)
-  /*! \brief true if s is one of this checkpoint's snapshot halves */
-  bool IsSnapshot(const Serializable *s) const { return s == &half_[0] || s == &half_[1]; }
+  /*! \brief true if s is one of this checkpoint's snapshot slots */
+  bool IsSnapshot(const Serializable *s) const {
+    for (const auto &h : half_) {
+      if (s == &h) return true;
+    }
+    return false;
+  }
+  /*! \brief mirror policy: true = every checkpoint, false = when the side stream is idle */
+  void set_mirror_always(bool v) { mirror_always_ = v; }
+  /*! \brief checkpoints whose host mirror was started at snapshot time / deferred */
+  uint64_t mirrors() const { return mirrors_; }
+  uint64_t mirrors_deferred() const { return mirrors_deferred_; }
   /*! \brief the header of a snapshot: meta_len, meta, n, sizes (the payload format minus data) */
   void SaveHeader(const Serializable *snapshot, Stream *fo) const;
   /*! \brief HBM buffer i of a snapshot */
@@ -58,7 +73,7 @@ class DeviceCheckpoint {
   const std::vector<size_t> &loader_sizes() const { return loader_.nbytes; }
   /*! \brief the payload already reached the loader's buffers: its Load reads the header only */
   void MarkPayloadDelivered() { payload_delivered_ = true; }
-  /*! \brief bytes of HBM reserved by the two snapshot halves */
+  /*! \brief bytes of HBM reserved by the snapshot slots */
   size_t reserved_bytes() const;
 
  private:
@@ -71,6 +86,10 @@ class DeviceCheckpoint {
     char *pinned{nullptr};        // pinned host mirror
     size_t pinned_cap{0};
     hipEvent_t d2h_done{nullptr};
+    hipEvent_t snap_done{nullptr};  // the HBM snapshot of this slot is complete
+    mutable bool mirror_valid{false};  // pinned holds this snapshot (or its copy is queued)
+    /*! \brief queue the D2H mirror of this slot on the side stream */
+    void StartMirror() const;
     void Load(Stream *) override;
     void Save(Stream *fo) const override;
   };
@@ -83,9 +102,12 @@ class DeviceCheckpoint {
   };
   DevicePlane *plane_;
   hipStream_t side_{nullptr};
-  hipEvent_t snap_done_{nullptr};
-  Half half_[2];
-  int cur_{1};
+  static constexpr int kSlots = 3;
+  Half half_[kSlots];
+  int cur_{kSlots - 1};
+  bool mirror_always_{false};
+  const Half *last_mirror_{nullptr};  // slot of the most recently started mirror
+  uint64_t mirrors_{0}, mirrors_deferred_{0};
   LoaderImpl loader_;
   std::string loaded_meta_;
   bool loader_active_{false};

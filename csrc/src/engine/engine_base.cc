@@ -98,6 +98,15 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_host_out_of_place")) host_out_of_place_ = utils::StringToBool(val);
   if (is("rabit_device_world1_transport")) world1_transport_ = utils::StringToBool(val);
   if (is("rabit_host_shm")) shm_enabled_ = utils::StringToBool(val);
+  if (is("rabit_device_ckpt_mirror")) {
+    if (!strcmp(val, "always")) {
+      ckpt_mirror_always_ = true;
+    } else if (!strcmp(val, "idle")) {
+      ckpt_mirror_always_ = false;
+    } else {
+      utils::Error("rabit_device_ckpt_mirror must be always or idle (got %s)", val);
+    }
+  }
   if (is("rabit_host_shm_min")) shm_min_ = core::ParseUnit(name, val);
   if (is("rabit_host_shm_buffer")) shm_stage_ = core::ParseUnit(name, val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
@@ -707,7 +716,10 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
 int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                   std::string *meta) {
   utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
-  if (!dev_ckpt_) dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+  if (!dev_ckpt_) {
+    dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+    dev_ckpt_->set_mirror_always(ckpt_mirror_always_);
+  }
   const int version = this->LoadCheckPoint(dev_ckpt_->Loader(n, ptrs, nbytes), nullptr);
   if (version > 0 && meta != nullptr) *meta = dev_ckpt_->loaded_meta();
   return version;
@@ -747,7 +759,9 @@ std::string EngineBase::StatsJson() const {
   }
   os << ",\"n_allreduce\":" << s.n_allreduce << ",\"n_broadcast\":" << s.n_broadcast
      << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
-     << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_shm_ops\":" << s.n_shm_ops << ",\"n_recovered_ops\":" << s.n_recovered_ops
+     << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_shm_ops\":" << s.n_shm_ops
+     << ",\"ckpt_mirrors\":" << (dev_ckpt_ ? dev_ckpt_->mirrors() : 0)
+     << ",\"ckpt_mirrors_deferred\":" << (dev_ckpt_ ? dev_ckpt_->mirrors_deferred() : 0) << ",\"n_recovered_ops\":" << s.n_recovered_ops
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
      << ",\"n_device_replays\":" << s.n_device_replays

@@ -179,6 +179,7 @@ class EngineBase : public IEngine {
   // one-peer direct group) instead of the local short-cut, so their API paths run on one GPU
   bool world1_transport_{false};
   bool shm_enabled_{true};          // rabit_host_shm
+  bool ckpt_mirror_always_{false};  // rabit_device_ckpt_mirror=always: mirror every checkpoint
   size_t shm_min_{1u << 20};        // rabit_host_shm_min
   size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)
   bool calibrate_{true};
