@@ -226,6 +226,7 @@ RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t coun
 RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
   if (e == nullptr || e->device_plane() == nullptr) return nullptr;
+  rabit::device::DeviceGuard dg(e->device_plane()->device());
   return e->device_plane()->SymAlloc(nbytes);
 }
 

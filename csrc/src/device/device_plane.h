@@ -80,6 +80,29 @@ class DeviceArena {
   size_t chunk_{256u << 20}, cap_{size_t(64) << 30};
 };
 
+/*!
+ * \brief makes `device` current for a scope (allocations and launches of the plane go to its
+ *        GPU even if the calling thread switched devices in between), then restores it
+ */
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    if (device < 0) return;
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != device && hipSetDevice(device) == hipSuccess) {
+      prev_ = cur;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+
+ private:
+  int prev_{-1};
+};
+
 class DevicePlane {
  public:
   /*! \brief number of visible GPUs (0 when HIP has no device) */

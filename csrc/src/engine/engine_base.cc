@@ -245,6 +245,7 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec, const voi
       !(spec.op == mpi::kBitwiseOR && (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble))) {
     // large host buffer on a GPU node: stage through HBM and use the device transports (the
     // role of the reference's MPI engine: vendor collectives instead of TCP)
+    device::DeviceGuard dg(dev_->device());
     void *d = dev_->Scratch(bytes, 2);
     Status s = EnsureDeviceComm();
     if (s != Status::kSuccess) return s;
@@ -305,6 +306,7 @@ Status EngineBase::EnsureShm() {
 
 Status EngineBase::EnsureDeviceComm() {
   utils::Check(dev_ != nullptr, "device buffer given but the device plane is disabled");
+  device::DeviceGuard dg(dev_->device());
   if (dev_->ready()) return Status::kSuccess;
   const int n = GetWorldSize();
   // 1. every rank describes its GPU (and exports its peer buffers when the direct transport
@@ -469,6 +471,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   const size_t bytes = spec.bytes();
   if (bytes == 0) return Status::kSuccess;
   if (dst2 == dst) dst2 = nullptr;
+  device::DeviceGuard dg(dev_->device());
   bool rccl_ok = spec.builtin() && spec.dtype <= mpi::kULongLong;
   if (spec.builtin() && spec.op == mpi::kBitwiseOR &&
       (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble)) {
@@ -541,6 +544,7 @@ Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
     return host_->TreeBroadcast(buf, size, root);
   }
   if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
+  device::DeviceGuard dg(dev_->device());
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
@@ -578,6 +582,7 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
     return host_->RingAllgather(buf, total, begin, end, prev_size);
   }
   if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
+  device::DeviceGuard dg(dev_->device());
   // every rank needs every slice: exchange (begin, size) pairs over the host ring first
   const int n = GetWorldSize();
   std::vector<uint64_t> meta(2 * n, 0);
@@ -707,7 +712,11 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
   for (int i = 0; i < n; ++i) {
     utils::Check(nbytes[i] == 0 || OnDevice(ptrs[i]), "device checkpoint: buffer %d not in HBM", i);
   }
-  if (!dev_ckpt_) dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+  device::DeviceGuard dg(dev_->device());
+  if (!dev_ckpt_) {
+    dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
+    dev_ckpt_->set_mirror_always(ckpt_mirror_always_);
+  }
   trace::Scope ts("device_snapshot", rank_, version_number_, seq_counter_, 0, 1);
   const Serializable *snap = dev_ckpt_->Snapshot(n, ptrs, nbytes, meta);
   this->LazyCheckPoint(snap);
@@ -716,6 +725,7 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
 int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                   std::string *meta) {
   utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
+  device::DeviceGuard dg(dev_->device());
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_always(ckpt_mirror_always_);

@@ -340,6 +340,7 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
     s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
     if (s != Status::kSuccess) return s;
     if (v[0] == 1 && v[1] != std::numeric_limits<int>::max()) {
+      device::DeviceGuard dg(dev_->device());
       s = EnsureDeviceComm();
       if (s != Status::kSuccess) return s;
       const int root = v[1];
@@ -426,6 +427,7 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
   Status s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
   if (v[0] != 1 || v[1] == std::numeric_limits<int>::max()) return Status::kAborted;
+  device::DeviceGuard dg(dev_->device());
   const int root = v[1];
   std::string hdr;
   if (rank_ == root) {
