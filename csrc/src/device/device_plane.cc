@@ -258,6 +258,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
         new PeerGroup(device_, cfg_.peer_stage, cfg_.peer_deadline_sec, stream_, heap_));
     if (cfg_.phase_timing) peers_->EnableTiming();
     peers_->set_oneshot_max(cfg_.oneshot_max);
+    peers_->set_push(cfg_.direct_mode == 2);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();

@@ -51,6 +51,7 @@ struct DeviceConfig {
   bool ops_on_user_stream{true};       // enqueue collectives on the caller's stream
   size_t sym_heap{0};                  // bytes of the symmetric (IPC-exported) heap, 0: none
   size_t oneshot_max{256u << 10};      // direct allreduce: one-shot up to this many bytes
+  int direct_mode{0};                  // direct reduce-scatter: 0 calibrated, 1 pull, 2 push
 };
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
@@ -157,6 +158,12 @@ class DevicePlane {
   size_t direct_min_bytes() const { return cfg_.direct_min_bytes; }
   /*! \brief calibration: -1 normal routing, 0 force RCCL, 1 force direct */
   void ForceTransport(int which) { force_ = which; }
+  /*! \brief direct reduce-scatter by remote writes (push) instead of remote reads */
+  void SetDirectPush(bool v) {
+    if (peers_ != nullptr) peers_->set_push(v);
+  }
+  bool direct_push() const { return peers_ != nullptr && peers_->push(); }
+  uint64_t push_chunks() const { return peers_ ? peers_->push_chunks() : 0; }
   /*! \brief barrier deadline of the direct transport (calibration runs with a short one) */
   void SetPeerDeadline(double sec) {
     if (peers_ != nullptr) peers_->set_deadline_sec(sec);

@@ -247,11 +247,18 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     // from overwriting its input (second destination, the caller's next kernels) while a slower
     // peer is still reading it.  Two-shot reads all inputs before the second barrier.
     const bool oneshot = indirect && c * tn <= oneshot_max_ && count <= chunk;
-    const bool zero_copy = indirect && !oneshot && stage_prep == kPrepCopy &&
+    const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
+    // push: the owners' inboxes receive the input segments directly (n * seg <= chunk always
+    // holds: chunk is a multiple of 256 n)
+    const bool use_push = push_ && !oneshot && stage_prep == kPrepCopy &&
+                          n_ * seg * tn <= stage_bytes_;
+    const bool zero_copy = indirect && !oneshot && !use_push && stage_prep == kPrepCopy &&
                            InHeap(chunk_src, c * tn) &&
                            (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
     XRABIT_TRY_HIP(mark(0));
-    if (zero_copy) {
+    if (use_push) {
+      // no staging: this rank's own stage is its inbox, written by the peers
+    } else if (zero_copy) {
       ++zero_copy_chunks_;
     } else if (stage_prep == kPrepCopy) {
       XRABIT_TRY_HIP(LaunchCopy(mine, chunk_src, c * tn, stream_));
@@ -293,9 +300,45 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       ++oneshot_ops_;
       continue;
     }
-    const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
     SegRange(c, seg, rank_, &lo, &hi);
+    if (use_push) {
+      // segment q of this rank's input goes to inbox slot `rank_` of rank q's stage (posted
+      // remote writes, read from the input where it is), then every inbox is local memory
+      CopyBatch b;
+      NewBatch(&b);
+      for (int q = 0; q < n_; ++q) {
+        size_t qlo, qhi;
+        SegRange(c, seg, q, &qlo, &qhi);
+        AddSeg(&b, stage(q, which) + (static_cast<size_t>(rank_) * seg) * tn,
+               chunk_src + qlo * tn, nullptr, (qhi - qlo) * tn);
+      }
+      if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+      XRABIT_TRY_HIP(Barrier());
+      XRABIT_TRY_HIP(mark(2));
+      if (hi > lo) {
+        const void *srcs[kMaxPeers];
+        for (int p = 0; p < n_; ++p) srcs[p] = mine + (static_cast<size_t>(p) * seg) * tn;
+        // the result lands in this rank's own slot, where the gather of every peer reads it
+        XRABIT_TRY_HIP(step(mine + (static_cast<size_t>(rank_) * seg) * tn, srcs, n_, hi - lo,
+                            dev_status(), nullptr, post_scale ? alpha : 0.0, stream_));
+      }
+      XRABIT_TRY_HIP(mark(3));
+      XRABIT_TRY_HIP(Barrier());
+      XRABIT_TRY_HIP(mark(4));
+      NewBatch(&b);
+      for (int p = 0; p < n_; ++p) {
+        size_t plo, phi;
+        SegRange(c, seg, p, &plo, &phi);
+        const size_t at = (off + plo) * tn;
+        AddSeg(&b, out + at, stage(p, which) + (static_cast<size_t>(p) * seg) * tn,
+               out2 != nullptr ? out2 + at : nullptr, (phi - plo) * tn);
+      }
+      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+      XRABIT_TRY_HIP(mark(5));
+      ++push_chunks_;
+      continue;
+    }
     if (indirect) {
       ResolveArgs ra{};
       ra.my_mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(

@@ -14,6 +14,9 @@
  *    in place with the multi-source kernel; barrier; everyone gathers the n reduced segments
  *    (optionally storing them twice: result log + user buffer).  Per rank, 2(n-1)/n of the
  *    payload crosses xGMI — the bandwidth-optimal amount — spread over all links.
+ *    Push variant (set_push): every rank writes segment q of its input straight into rank q's
+ *    stage (an inbox slot per sender); barrier; rank r reduces its n local inbox slots;
+ *    barrier; everyone gathers as above.  The calibration picks pull or push per machine.
  *  - Broadcast: root stages; barrier; rank p pulls segment p from the root; barrier; everyone
  *    pulls the other segments from their owners (scatter + allgather: the root's links carry
  *    2/n of the payload each instead of all of it).
@@ -153,6 +156,15 @@ class PeerGroup {
   uint64_t zero_copy_chunks() const { return zero_copy_chunks_; }
   /*! \brief ops of at most this many bytes use the one-shot allreduce (one barrier) */
   void set_oneshot_max(size_t b) { oneshot_max_ = b; }
+  /*!
+   * \brief reduce-scatter by remote WRITES (push) instead of remote reads: every rank writes
+   *        segment q of its input into an inbox slot of rank q's stage buffer, then reduces
+   *        its inbox locally; the gather still pulls.  Posted writes need no round trip per
+   *        request over xGMI; which variant is faster is measured by the calibration.
+   */
+  void set_push(bool v) { push_ = v; }
+  bool push() const { return push_; }
+  uint64_t push_chunks() const { return push_chunks_; }
   uint64_t oneshot_ops() const { return oneshot_ops_; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
@@ -205,6 +217,8 @@ class PeerGroup {
   uint64_t zero_copy_chunks_{0};
   size_t oneshot_max_{256u << 10};
   uint64_t oneshot_ops_{0};
+  bool push_{false};
+  uint64_t push_chunks_{0};
 };
 
 }  // namespace device

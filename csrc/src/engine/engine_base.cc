@@ -91,6 +91,17 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
   if (is("rabit_device_oneshot_max")) dcfg_.oneshot_max = core::ParseUnit(name, val);
+  if (is("rabit_device_direct_mode")) {
+    if (!strcmp(val, "auto")) {
+      dcfg_.direct_mode = 0;
+    } else if (!strcmp(val, "pull")) {
+      dcfg_.direct_mode = 1;
+    } else if (!strcmp(val, "push")) {
+      dcfg_.direct_mode = 2;
+    } else {
+      utils::Error("rabit_device_direct_mode must be auto, pull or push (got %s)", val);
+    }
+  }
   if (is("rabit_device_symmetric_heap")) dcfg_.sym_heap = core::ParseUnit(name, val);
   if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
@@ -418,10 +429,36 @@ Status EngineBase::CalibrateDevice() {
     for (size_t i = 0; i < sizes[k] && ok; ++i) ok = host[i] == want ? 1 : 0;
     if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
   }
+  // 1b. the push variant of the direct reduce-scatter (remote writes) at the large size;
+  //     verified like the pull one.  A failed run disables the direct transport altogether (a
+  //     failed barrier drops the group); a wrong result only rules push out.
+  int push_ok = ok && dcfg_.direct_mode == 0 ? 1 : 0;
+  double t_push = 0;
+  if (push_ok) {
+    const double t_pull = t[1][1];
+    dev_->SetDirectPush(true);
+    Status st;
+    if (!measure(1, 1, &st)) {
+      ok = 0;
+      push_ok = 0;
+    } else {
+      t_push = t[1][1];
+      host.resize(sizes[1]);
+      dev_->StageToHost(host.data(), dst, sizes[1] * 4);
+      const float want = 0.5f * n * (n + 1);
+      for (size_t i = 0; i < sizes[1] && push_ok; ++i) push_ok = host[i] == want ? 1 : 0;
+      if (!push_ok) utils::HandleLogInfo("[%d] direct push verification failed\n", rank_);
+    }
+    t[1][1] = t_pull;
+    if (dev_->has_peers()) dev_->SetDirectPush(false);
+  }
   dev_->ForceTransport(-1);
   dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
-  Status s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  int flags[2] = {ok, push_ok};
+  Status s = host_->Allreduce(flags, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
+  ok = flags[0];
+  push_ok = flags[1];
   // 2. RCCL (only worth timing when the direct transport is usable: the choice is uniform)
   if (ok) {
     for (int k = 0; k < 2; ++k) {
@@ -434,13 +471,17 @@ Status EngineBase::CalibrateDevice() {
     dev_->ForceTransport(-1);
   }
   // identical decision everywhere: max time over ranks
-  double agg[4] = {t[0][0], t[0][1], t[1][0], t[1][1]};
-  s = host_->Allreduce(agg, sizeof(double), 4, coll::HostReducer(mpi::kDouble, mpi::kMax));
+  double agg[5] = {t[0][0], t[0][1], t[1][0], t[1][1], t_push};
+  s = host_->Allreduce(agg, sizeof(double), 5, coll::HostReducer(mpi::kDouble, mpi::kMax));
   if (s != Status::kSuccess) return s;
   size_t threshold = static_cast<size_t>(-1);
   if (!ok) {
     dev_->DropPeers();
   } else {
+    // pull or push for the two-shot path: the faster one at the large size (same everywhere)
+    const bool use_push = push_ok && agg[4] < agg[3];
+    dev_->SetDirectPush(use_push);
+    if (use_push) agg[3] = agg[4];
     // linear model t = a + b * bytes per transport through the two points; direct from the
     // crossover on (when its slope is smaller)
     const double x0 = sizes[0] * 4.0, x1 = sizes[1] * 4.0;
@@ -453,12 +494,13 @@ Status EngineBase::CalibrateDevice() {
     dev_->set_direct_min_bytes(threshold);
   }
   calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
-            static_cast<double>(sizes[1] * 4)};
+            static_cast<double>(sizes[1] * 4), agg[4]};
   if (debug_ || rank_ == 0) {
     utils::HandleLogInfo(
         "[xrabit] device calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B rccl "
-        "%.1f us direct %.1f us -> direct %s\n",
+        "%.1f us direct %.1f us (push %.1f us, %s) -> direct %s\n",
         n, sizes[0] * 4, agg[0] * 1e6, agg[2] * 1e6, sizes[1] * 4, agg[1] * 1e6, agg[3] * 1e6,
+        agg[4] * 1e6, dev_->direct_push() ? "push" : "pull",
         !ok ? "disabled (failed verification)"
             : (threshold == static_cast<size_t>(-1) ? "off (RCCL faster)"
                                                     : ("from " + std::to_string(threshold) + " B").c_str()));
@@ -759,7 +801,10 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_direct_min\":"
      << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
-     << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]";
+     << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
+     << ",\"calib_push_us\":" << calib_.push_big * 1e6
+     << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
+     << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0);
   double phase[device::PeerGroup::kPhases];
   uint64_t nphase = 0;
   if (dev_ && dev_->DirectPhaseUs(phase, &nphase)) {

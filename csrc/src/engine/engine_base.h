@@ -187,10 +187,11 @@ class EngineBase : public IEngine {
   bool device_replay_{true};       // recover HBM results with a device broadcast
   bool host_via_device_{false};     // stage large host-buffer allreduces through HBM
   size_t host_dev_min_{1u << 20};
-  /*! \brief last calibration: rccl small/big, direct small/big (s), small/big bytes */
+  /*! \brief last calibration: rccl small/big, direct small/big (s; direct big = the chosen
+   *  variant), small/big bytes, push variant at the big size */
   struct {
-    double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes;
-  } calib_{0, 0, 0, 0, 0, 0};
+    double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes, push_big;
+  } calib_{0, 0, 0, 0, 0, 0, 0};
   bool trace_spans_{false};
   bool trace_roctx_{false};
   size_t trace_capacity_{1 << 16};

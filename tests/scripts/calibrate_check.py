@@ -22,5 +22,9 @@ thr = st["device_direct_min"]
 lo = rabit.allreduce(np.array([thr]), rabit.MIN)[0]
 hi = rabit.allreduce(np.array([thr]), rabit.MAX)[0]
 assert lo == hi, (lo, hi)
+# the push variant was timed and the pull/push choice is the same everywhere
+assert st["calib_push_us"] > 0, st
+push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
+assert push in (0, world), push
 rabit.finalize()
 print("[%d] CALIB OK thr=%s calib=%s" % (rank, thr, calib), flush=True)

@@ -102,6 +102,8 @@ assert torch.equal(buf.cpu(), exp), "allgatherv"
 stats = rabit.stats()
 assert stats["device_direct"] == 1 and stats["device_rccl"] == 0, stats
 assert stats["oneshot_ops"] > 0, stats  # the small cases took the one-shot path
+if "rabit_device_direct_mode=push" in sys.argv:
+    assert stats["direct_push"] == 1 and stats["push_chunks"] > 0, stats
 
 # a rough number for the log: 64 MiB fp32 sum, all ranks' traffic on the one shared GPU
 x = torch.ones(16 << 20, device=dev)

@@ -30,11 +30,22 @@ def test_direct_collectives(world):
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
 
-@pytest.mark.parametrize("mock", [[], ["mock=1,1,0,0"], ["mock=0,2,1,0", "mock=2,1,2,0"]])
-def test_direct_recovery(mock):
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_direct_collectives_push(world):
+    """the push (remote-write) reduce-scatter variant of the two-shot allreduce"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("device_ft.py", 3, mock, attempts=4)
+    rc, out = _run("device_multi.py", world, ["rabit_device_direct_mode=push"])
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVMULTI OK") == world, out[-3000:]
+
+
+@pytest.mark.parametrize("mock", [[], ["mock=1,1,0,0"], ["mock=0,2,1,0", "mock=2,1,2,0"]])
+@pytest.mark.parametrize("mode", ["pull", "push"])
+def test_direct_recovery(mock, mode):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_ft.py", 3, mock + ["rabit_device_direct_mode=" + mode], attempts=4)
     assert rc == 0, out[-5000:]
     assert out.count("DEVFT OK") == 3, out[-3000:]
     if mock:
