@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstring>
 
+#include "core/wait_state.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -132,6 +133,7 @@ char *ShmGroup::stage(int r, int which) const {
 }
 
 Status ShmGroup::Barrier(const Probe &probe) {
+  core::WaitScope waiting;
   const uint64_t e = ++epoch_;
   // release: this rank's stage writes before the arrival flag, in every peer's header
   for (int p = 0; p < n_; ++p) __atomic_store_n(Flag(peer_[p], rank_), e, __ATOMIC_RELEASE);

@@ -1,0 +1,80 @@
+/*!
+ * \file wait_state.h
+ * \brief Where this process is while inside a collective: waiting on peers / the device / the
+ *        tracker, or working.  The hang watchdog (rabit_hang_timeout_sec) uses it to tell a
+ *        rank that is stuck in its own code inside an op (its peers then wait for it forever:
+ *        the reference cannot recover from that) from the ranks that merely wait for it.
+ *
+ * A rank that has been *working* — inside an op and not in any wait — for longer than the hang
+ * timeout exits with a restartable status; its peers see the connection reset and run the
+ * normal recovery, replaying what the restarted rank missed.  Ranks that wait never fire.
+ * Process-wide state: an engine is driven by one thread at a time.
+ */
+#ifndef XRABIT_CORE_WAIT_STATE_H_
+#define XRABIT_CORE_WAIT_STATE_H_
+
+#include <atomic>
+#include <chrono>
+
+namespace rabit {
+namespace core {
+
+inline double MonotonicSec() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+struct WaitState {
+  std::atomic<int> op_depth{0};        // > 0: inside a public collective / checkpoint
+  std::atomic<int> wait_depth{0};      // > 0: blocked on peers, the device or the tracker
+  std::atomic<double> working_since{0};  // start of the current working stretch (0: none)
+};
+
+inline WaitState &GlobalWaitState() {
+  static WaitState s;
+  return s;
+}
+
+/*! \brief marks a public operation; the working stretch starts when it is entered */
+class OpScope {
+ public:
+  OpScope() {
+    WaitState &w = GlobalWaitState();
+    if (w.op_depth.fetch_add(1) == 0 && w.wait_depth.load() == 0) {
+      w.working_since.store(MonotonicSec());
+    }
+  }
+  ~OpScope() {
+    WaitState &w = GlobalWaitState();
+    if (w.op_depth.fetch_sub(1) == 1) w.working_since.store(0.0);
+  }
+  OpScope(const OpScope &) = delete;
+  OpScope &operator=(const OpScope &) = delete;
+};
+
+/*! \brief marks a blocking wait on something outside this rank */
+class WaitScope {
+ public:
+  WaitScope() {
+    WaitState &w = GlobalWaitState();
+    w.wait_depth.fetch_add(1);
+    w.working_since.store(0.0);
+  }
+  ~WaitScope() {
+    WaitState &w = GlobalWaitState();
+    if (w.wait_depth.fetch_sub(1) == 1 && w.op_depth.load() > 0) {
+      w.working_since.store(MonotonicSec());
+    }
+  }
+  WaitScope(const WaitScope &) = delete;
+  WaitScope &operator=(const WaitScope &) = delete;
+};
+
+/*! \brief seconds this rank has been working inside an op without waiting (0: not) */
+inline double WorkingFor() {
+  const double since = GlobalWaitState().working_since.load();
+  return since > 0 ? MonotonicSec() - since : 0.0;
+}
+}  // namespace core
+}  // namespace rabit
+#endif  // XRABIT_CORE_WAIT_STATE_H_

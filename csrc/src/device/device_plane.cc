@@ -12,6 +12,7 @@
 #include <cstring>
 #include <thread>
 
+#include "core/wait_state.h"
 #include "device/kernels.h"
 #include "rabit/internal/utils.h"
 
@@ -311,6 +312,7 @@ void DevicePlane::EnterFromUser() {
 }
 
 Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
+  core::WaitScope waiting;  // peers' barriers and RCCL: waiting on other ranks
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   for (uint64_t iter = 0;; ++iter) {
@@ -373,7 +375,10 @@ Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
   return s;
 }
 
-void DevicePlane::Synchronize() { CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
+void DevicePlane::Synchronize() {
+  core::WaitScope waiting;
+  CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
 
 void DevicePlane::CopyAsync(void *dst, const void *src, size_t bytes) {
   if (bytes == 0 || dst == src) return;

@@ -395,15 +395,24 @@ Status EngineBase::CalibrateDevice() {
   int ok = 1;
   dev_->SetPeerDeadline(5.0);
   std::vector<float> host;
-  // timed allreduce of sizes[k] on the forced transport; false on failure
+  constexpr int kCalibReps = 4;
+  // the value every rank must hold after the last repetition
+  const float want = 0.5f * n * (n + 1) + 16.0f * (kCalibReps - 1) * n;
+  // Timed allreduce of sizes[k] on the forced transport; false on failure.  Every repetition
+  // reduces different values (rank + 1 + 16 rep), so the check of the last one also catches a
+  // peer mapping that serves stale bytes of the previous op on the same stage buffer (the
+  // buffers alternate, so rep 3 reuses rep 1's), not only a broken one.
   auto measure = [&](int which, int k, Status *st) {
     const size_t count = sizes[k];
-    device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, rank_ + 1.0, dev_->stream()),
-                     "LaunchFill");
     // test hook: without RCCL (ranks sharing a GPU) the "RCCL" leg runs direct as well
     dev_->ForceTransport(which == 0 && !dev_->has_comm() ? 1 : which);
     double best = 1e30;
-    for (int rep = 0; rep < 4; ++rep) {
+    for (int rep = 0; rep < kCalibReps; ++rep) {
+      device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, rank_ + 1.0 + 16.0 * rep,
+                                          dev_->stream()),
+                       "LaunchFill");
+      *st = dev_->Finish(MakeProbe());
+      if (*st != Status::kSuccess) return false;
       const double t0 = utils::GetTime();
       *st = dev_->Allreduce(src, dst, nullptr, count, mpi::kFloat, mpi::kSum, device::kPrepCopy,
                             1.0, MakeProbe());
@@ -425,7 +434,6 @@ Status EngineBase::CalibrateDevice() {
     // verify the direct result on the host: a broken peer mapping must not go unnoticed
     host.resize(sizes[k]);
     dev_->StageToHost(host.data(), dst, sizes[k] * 4);
-    const float want = 0.5f * n * (n + 1);
     for (size_t i = 0; i < sizes[k] && ok; ++i) ok = host[i] == want ? 1 : 0;
     if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
   }
@@ -445,7 +453,6 @@ Status EngineBase::CalibrateDevice() {
       t_push = t[1][1];
       host.resize(sizes[1]);
       dev_->StageToHost(host.data(), dst, sizes[1] * 4);
-      const float want = 0.5f * n * (n + 1);
       for (size_t i = 0; i < sizes[1] && push_ok; ++i) push_ok = host[i] == want ? 1 : 0;
       if (!push_ok) utils::HandleLogInfo("[%d] direct push verification failed\n", rank_);
     }

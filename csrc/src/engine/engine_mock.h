@@ -21,6 +21,7 @@
 #include <thread>
 #include <tuple>
 
+#include "core/wait_state.h"
 #include "engine/engine_robust.h"
 #include "rabit/internal/timer.h"
 
@@ -163,6 +164,7 @@ class EngineMock : public EngineRobust {
     if (it == mock_map_.end()) return;
     num_trial_ += 1;
     if (it->second == 2) {
+      core::OpScope in_op;  // the hang is inside the collective (rabit_hang_timeout_sec)
       fprintf(stderr, "[%d]@@@Hit Mock Hang:%s\n", rank_, what);
       fflush(stderr);
       for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));

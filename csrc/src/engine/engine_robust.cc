@@ -15,6 +15,7 @@
 #include <cstring>
 
 #include "core/trace.h"
+#include "core/wait_state.h"
 #include "device/kernels.h"
 #include "rabit/internal/io.h"
 #include "rabit/internal/timer.h"
@@ -151,6 +152,10 @@ void EngineRobust::SetParam(const char *name, const char *val) {
   if (!strcmp(name, "rabit_global_replica")) num_global_replica_ = atoi(val);
   if (!strcmp(name, "rabit_local_replica")) num_local_replica_ = atoi(val);
   if (!strcmp(name, "rabit_elide_consensus")) elide_consensus_ = utils::StringToBool(val);
+  if (!strcmp(name, "rabit_hang_timeout_sec")) {
+    hang_timeout_sec_ = atof(val);
+    utils::Check(hang_timeout_sec_ >= 0, "rabit_hang_timeout_sec should be non negative");
+  }
 }
 
 bool EngineRobust::Init(int argc, char *argv[]) {
@@ -160,7 +165,7 @@ bool EngineRobust::Init(int argc, char *argv[]) {
   result_buffer_round_ =
       num_global_replica_ == 0 ? -1 : std::max(GetWorldSize() / num_global_replica_, 1);
   if (dev_) resbuf_.SetArena(dev_->arena());
-  if (timeout_enabled_) StartWatchdog();
+  if (timeout_enabled_ || hang_timeout_sec_ > 0) StartWatchdog();
   return true;
 }
 
@@ -271,6 +276,7 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
                                  void *prepare_arg, const char *_file, const int _line,
                                  const char *_caller, const void *prep_src, int prep_op,
                                  double prep_alpha) {
+  core::OpScope op_scope;
   const bool dev = OnDevice(buf);
   const size_t bytes = spec.bytes();
   auto run_prepare = [&]() {
@@ -352,6 +358,7 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
 
 void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char *_file,
                              const int _line, const char *_caller) {
+  core::OpScope op_scope;
   if (GetWorldSize() == 1 && world1_fastpath_) return;
   if (total_size == 0) return;
   const bool dev = OnDevice(buf);
@@ -405,6 +412,7 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
 void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, size_t slice_end,
                              size_t size_prev_slice, const char *_file, const int _line,
                              const char *_caller) {
+  core::OpScope op_scope;
   if (GetWorldSize() == 1 && world1_fastpath_) return;
   if (total_size == 0) return;
   const bool dev = OnDevice(buf);
@@ -474,6 +482,7 @@ void EngineRobust::LocalModelCheck(bool with_local) {
 }
 
 int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local_model) {
+  core::OpScope op_scope;
   checkpoint_loaded_ = true;
   if (GetWorldSize() == 1 && world1_fastpath_) return 0;
   LocalModelCheck(local_model != nullptr);
@@ -533,6 +542,7 @@ int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local
 
 void EngineRobust::CheckPointImpl(const Serializable *global_model,
                                   const Serializable *local_model, bool lazy) {
+  core::OpScope op_scope;
   if (GetWorldSize() == 1 && world1_fastpath_) {
     version_number_ += 1;
     return;
@@ -661,8 +671,22 @@ void EngineRobust::WatchdogLoop() {
     // understands (steady-clock waits use pthread_cond_clockwait, invisible to gcc-11 TSan)
     wd_cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100));
     if (wd_stop_) break;
+    // a rank stuck in its own code inside an op (a prepare function or Save that never
+    // returns): its peers only wait for it, so nobody else can notice.  Leaving with a
+    // restartable status turns the hang into an ordinary failure: the peers see the links
+    // drop and recover, and the restarted rank replays what it missed.
+    const double working = core::WorkingFor();
+    if (hang_timeout_sec_ > 0 && working > hang_timeout_sec_) {
+      fprintf(stderr,
+              "[%d] xrabit: working inside a collective for %.1f s without waiting on peers "
+              "(rabit_hang_timeout_sec=%g): exiting for a restart\n",
+              wd_rank_.load(), working, hang_timeout_sec_);
+      fflush(stderr);
+      std::_Exit(kHangExitCode);
+    }
     const double since = recovering_since_.load();
-    if (since > 0 && utils::GetTime() - since > timeout_sec_ && !watchdog_fired_.load()) {
+    if (timeout_enabled_ && since > 0 && utils::GetTime() - since > timeout_sec_ &&
+        !watchdog_fired_.load()) {
       watchdog_fired_.store(true);
       // unblock whatever this rank is waiting on, then apply the timeout action
       abort_flag_.store(true);

@@ -71,6 +71,8 @@ class EngineRobust : public EngineBase {
   /*! \brief called when the watchdog expires (default: log and terminate the process) */
   typedef void (*TimeoutHandler)(int rank, int timeout_sec);
   void SetTimeoutHandler(TimeoutHandler h) { timeout_handler_ = h; }
+  /*! \brief exit status of a rank that rabit_hang_timeout_sec found stuck inside an op */
+  static constexpr int kHangExitCode = 252;
   /*! \brief feed CheckAndRecover directly (tests); returns its result */
   bool TestCheckAndRecover(Status s) { return CheckAndRecover(s); }
   bool watchdog_fired() const { return watchdog_fired_.load(); }
@@ -238,6 +240,7 @@ class EngineRobust : public EngineBase {
   std::atomic<double> recovering_since_{0.0};
   std::atomic<bool> watchdog_fired_{false};
   std::atomic<int> wd_rank_{-1};  // rank as seen by the watchdog thread (rank_ is not atomic)
+  double hang_timeout_sec_{0};    // rabit_hang_timeout_sec (0: off)
 };
 }  // namespace engine
 }  // namespace rabit

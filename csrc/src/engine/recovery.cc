@@ -22,6 +22,7 @@
 #include <utility>
 
 #include "core/trace.h"
+#include "core/wait_state.h"
 #include "engine/engine_robust.h"
 #include "rabit/internal/io.h"
 #include "rabit/internal/timer.h"
@@ -55,7 +56,10 @@ bool EngineRobust::CheckAndRecover(Status s) {
   // simplest consistent repair: drop every link so the failure propagates, then rejoin
   for (auto &l : topo_.links) l->sock.Close();
   // spread the reconnect load on the tracker
-  std::this_thread::sleep_for(std::chrono::milliseconds(10 * std::max(rank_, 0)));
+  {
+    core::WaitScope waiting;
+    std::this_thread::sleep_for(std::chrono::milliseconds(10 * std::max(rank_, 0)));
+  }
   ReconnectLinks("recover");
   wd_rank_.store(rank_);
   stats_.t_recover += utils::GetTime() - t0;

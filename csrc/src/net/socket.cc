@@ -16,6 +16,7 @@
 
 #include <cstring>
 
+#include "core/wait_state.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -165,6 +166,7 @@ int TcpSocket::AtMark() const {
 }
 
 size_t TcpSocket::SendAll(const void *buf, size_t len) {
+  core::WaitScope waiting;
   const char *p = static_cast<const char *>(buf);
   size_t done = 0;
   while (done < len) {
@@ -184,6 +186,7 @@ size_t TcpSocket::SendAll(const void *buf, size_t len) {
 }
 
 size_t TcpSocket::RecvAll(void *buf, size_t len) {
+  core::WaitScope waiting;
   char *p = static_cast<char *>(buf);
   size_t done = 0;
   while (done < len) {
@@ -246,6 +249,7 @@ short Poller::Revents(int fd) const {
 }
 
 int Poller::Poll(int timeout_ms) {
+  core::WaitScope waiting;
   for (auto &p : fds_) p.revents = 0;
   int rc;
   do {

@@ -10,6 +10,7 @@
 #include <set>
 #include <vector>
 
+#include "core/wait_state.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -27,6 +28,7 @@ TcpSocket TrackerClient::Connect(int rank, int world_size) const {
     fprintf(stderr, "xrabit: retry connecting to tracker %s:%d (attempt %d)\n",
             cfg_->uri.c_str(), cfg_->port, attempt);
     // linear-exponential backoff as in the reference (sleep(retry << 1))
+    core::WaitScope waiting;
     sleep(static_cast<unsigned>(attempt << 1));
   }
   s.SendInt(kTrackerMagic);

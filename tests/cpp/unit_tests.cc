@@ -21,6 +21,7 @@
 
 #include "coll/host_coll.h"
 #include "core/params.h"
+#include "core/wait_state.h"
 #include "net/link_reset.h"
 #include "engine/engine_mock.h"
 #include "engine/engine_robust.h"
@@ -317,6 +318,35 @@ TEST(robust_shutdown_before_timeout) {
   EXPECT(r.Shutdown());
   std::this_thread::sleep_for(std::chrono::milliseconds(1200));
   EXPECT(g_timeouts.load() == 0);
+}
+
+TEST(wait_state_working_vs_waiting) {
+  using rabit::core::OpScope;
+  using rabit::core::WaitScope;
+  using rabit::core::WorkingFor;
+  EXPECT(WorkingFor() == 0.0);  // outside any op nothing counts
+  {
+    WaitScope w;  // a wait outside an op does not start a working stretch
+  }
+  EXPECT(WorkingFor() == 0.0);
+  {
+    OpScope op;
+    std::this_thread::sleep_for(std::chrono::milliseconds(30));
+    EXPECT(WorkingFor() >= 0.025);
+    {
+      OpScope nested;  // nested ops keep the outer stretch
+      EXPECT(WorkingFor() >= 0.025);
+      WaitScope w;
+      EXPECT(WorkingFor() == 0.0);  // waiting on peers: not working
+      {
+        WaitScope w2;
+      }
+      EXPECT(WorkingFor() == 0.0);  // still inside the outer wait
+    }
+    // the wait ended inside the op: a fresh stretch starts
+    EXPECT(WorkingFor() < 0.025);
+  }
+  EXPECT(WorkingFor() == 0.0);
 }
 
 // ---------------------------------------------------------------- public API, single node

@@ -87,3 +87,27 @@ def test_recover_shared_memory_transport(native_build, mode, kills):
     assert sum(a - 1 for a in job.attempts) >= 2
     import re
     assert all(int(k) > 0 for k in re.findall(r"PASSED shm_ops=(-?\d+)", out)), out[-2000:]
+
+
+def test_hang_in_prepare_becomes_a_recoverable_failure(native_build):
+    """rabit_hang_timeout_sec: a rank stuck in its own prepare function (not waiting on anyone)
+    exits for a restart; the job finishes with the same model as a clean run."""
+    script = os.path.join(ROOT, "tests", "scripts", "hang_prepare.py")
+    rc, job, out = _run([sys.executable, script, "rabit_hang_timeout_sec=2"], n=4, attempts=3,
+                        timeout=180)
+    assert rc == 0, out[-4000:]
+    assert out.count("DONE") == 4, out[-3000:]
+    assert "[2] prepare stuck" in out and "exiting for a restart" in out, out[-3000:]
+    assert job.attempts[2] == 2 and sum(job.attempts) == 5, job.attempts
+
+
+def test_mock_hang_detected_by_hang_timeout(native_build):
+    """mock_hang= freezes a rank inside a collective; the hang timeout turns it into a restart
+    and the reference's failure test passes on every rank."""
+    rc, job, out = _run([os.path.join(native_build, "recover_test"), "1000", "mode=global",
+                         "rabit_hang_timeout_sec=2", "mock_hang=3,1,1,0"], n=6, attempts=3,
+                        timeout=180)
+    assert rc == 0, out[-4000:]
+    assert out.count("PASSED") == 6, out[-4000:]
+    assert "Hit Mock Hang" in out and "exiting for a restart" in out, out[-3000:]
+    assert job.attempts[3] == 2, job.attempts
