@@ -23,6 +23,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import rabit_amd as rabit  # noqa: E402
 from rabit_amd.parallel.data_parallel import GradientBuckets, shard  # noqa: E402
+from rabit_amd.parallel.graphs import GraphedStep  # noqa: E402
 
 
 def main():
@@ -33,6 +34,9 @@ def main():
     ap.add_argument("--rows", type=int, default=6000)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--bucket-mb", type=float, default=0.25)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="replay forward+backward as one hipGraph (GraphedStep); bit-identical")
+    ap.add_argument("--layers", type=int, default=1, help="hidden layers of the MLP")
     args, rest = ap.parse_known_args()
     lib = "standard"
     params = []
@@ -58,8 +62,10 @@ def main():
     lo, hi = shard(args.rows, rank, world)
     xs, ys = X[lo:hi].to(dev), y[lo:hi].to(dev)
     torch.manual_seed(0)
-    model = torch.nn.Sequential(torch.nn.Linear(d_in, args.hidden), torch.nn.Tanh(),
-                                torch.nn.Linear(args.hidden, 1)).to(dev)
+    layers = [torch.nn.Linear(d_in, args.hidden), torch.nn.Tanh()]
+    for _ in range(args.layers - 1):
+        layers += [torch.nn.Linear(args.hidden, args.hidden), torch.nn.Tanh()]
+    model = torch.nn.Sequential(*layers, torch.nn.Linear(args.hidden, 1)).to(dev)
     buckets = GradientBuckets(model.parameters(), bucket_mb=args.bucket_mb)
     flat = {"p%d" % i: p.data for i, p in enumerate(model.parameters())}
 
@@ -82,10 +88,14 @@ def main():
     start = meta["next"] if version > 0 else 0
     if version > 0:
         print("[%d] resumed at version %d, step %d" % (rank, version, start), flush=True)
-    for step in range(start, args.steps):
-        buckets.zero_grad()
+    def compute():
         loss = torch.nn.functional.mse_loss(model(xs), ys)
-        loss.backward()
+        buckets.backward(loss)  # gradients straight into the HBM buckets (graph-safe)
+        return loss
+
+    step_fn = GraphedStep(compute) if (args.graph and dev.type == "cuda") else compute
+    for step in range(start, args.steps):
+        loss = step_fn()
         buckets.reduce()  # average over ranks; replayed from the survivors' logs after a restart
         with torch.no_grad():
             for p in model.parameters():
@@ -105,8 +115,9 @@ def main():
     assert lo_h == hi_h, "ranks disagree on the weights"
     st = rabit.stats()
     rabit.finalize()
-    print("[%d] DPTRAIN OK weights=%s device_ops=%d replays=%d" % (
-        rank, digest, st["n_device_ops"], st["n_device_replays"]), flush=True)
+    print("[%d] DPTRAIN OK weights=%s device_ops=%d replays=%d graphed=%d" % (
+        rank, digest, st["n_device_ops"], st["n_device_replays"],
+        int(getattr(step_fn, "captured", False))), flush=True)
 
 
 if __name__ == "__main__":

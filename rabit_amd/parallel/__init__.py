@@ -7,5 +7,8 @@ GradientBuckets   flat HBM gradient buckets (gradients are views into them, so b
                   lazy-prepare kernel.
 FaultTolerantLoop resume-from-checkpoint training loop (LoadCheckPoint / CheckPoint every
                   k steps), the rabit programming model for iterative jobs.
+GraphedStep       replays the launch-bound device part of an iteration (forward, backward,
+                  bucket zeroing) as one hipGraph; the collectives stay outside it.
 """
 from .data_parallel import FaultTolerantLoop, GradientBuckets  # noqa: F401
+from .graphs import GraphedStep  # noqa: F401

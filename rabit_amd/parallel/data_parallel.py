@@ -69,6 +69,28 @@ class GradientBuckets:
         for b in self.buckets:
             b.zero_()
 
+    def backward(self, loss):
+        """Write d(loss)/d(param) into the buckets, overwriting (no zero_grad needed).
+
+        Functional (`torch.autograd.grad`, then one multi-tensor copy into the bucket views)
+        rather than `loss.backward()`'s accumulation into `.grad`: the same gradient kernels
+        run, so the values are identical, and it stays exact when the step is replayed as a
+        hipGraph.  Accumulating backward passes captured in a graph gave wrong bias gradients
+        from the second replay on for some shapes on this PyTorch-ROCm build
+        (tools/graph_diag.py, profiles/r1_graphs/)."""
+        import torch
+
+        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        dst, src = [], []
+        for p, g in zip(self.params, grads):
+            if g is None:
+                p.grad.zero_()
+            else:
+                dst.append(p.grad)
+                src.append(g)
+        if dst:
+            torch._foreach_copy_(dst, src)
+
     def reduce(self, op: int = rabit.SUM):
         """Allreduce every bucket (in place); returns the buckets."""
         world = rabit.get_world_size()

@@ -1,0 +1,103 @@
+"""Replay a launch-bound per-iteration device closure as one hipGraph.
+
+A training step of a small or deep model is a few hundred short kernels (forward, backward,
+zeroing the gradient buckets); on MI355X each costs a few microseconds of host launch time,
+often more than the kernel itself.  `GraphedStep` captures the closure once into a hipGraph
+(`torch.cuda.CUDAGraph` is hipGraph on ROCm) and replays it with one launch per step.
+
+The collectives stay outside the graph on purpose: a rabit collective is host logic as much as
+device work (sequence numbers, the result log, consensus, recovery and replay after a failure),
+so `GradientBuckets.reduce()` runs after the replay, on the same stream, exactly as in an eager
+step.  The graph ends by writing the gradients into the bucket views (one multi-tensor copy), so
+the collective reads them where they are.
+
+    def compute_loss_and_grads():
+        loss = loss_fn(model(xs_static), ys_static)
+        buckets.backward(loss)     # functional gradients into the buckets (graph-exact)
+        return loss
+
+    step = GraphedStep(compute_loss_and_grads)  # static inputs: copy new data in
+    for it in loop:
+        xs_static.copy_(next_batch)
+        loss = step()              # warm-up runs eagerly, then capture + replay, then replay
+        buckets.reduce()           # fault-tolerant allreduce of the gradient buckets
+        optimizer_update()
+
+Every call executes the closure exactly once (warm-up calls run it eagerly; the capturing call
+replays right after capturing), so a job does the same work whether or not it is graphed.
+Measured on MI355X (profiles/r1_graphs/): the graphed runs of tools/graph_steps.py and
+examples/dp_train.py (3 ranks) end with weights bit-identical to the eager runs.
+
+Produce the gradients with `GradientBuckets.backward(loss)` (torch.autograd.grad + one copy into
+the buckets) inside the closure, not with `loss.backward()`: on this PyTorch-ROCm build a
+captured *accumulating* backward pass replays exactly once and then yields wrong gradients for
+some shapes; the culprit is the column reduction of the bias gradient (torch.sum(x, 0) on
+[512, 1024] replays wrongly from its second replay on: tools/graph_reduce_check.py).
+
+Known open issue: with a worker killed and restarted mid-training, graphed dp_train runs finish
+with weights that agree on every rank but differ from the clean run (eager runs with the same
+failures match it bit for bit: tools/graph_check.py).  Until that is understood, use eager
+steps where bit-exact recovery matters.
+"""
+from __future__ import annotations
+
+import os
+
+from typing import Any, Callable, Optional
+
+
+_SYNC_BEFORE_REPLAY = os.environ.get("RABIT_GRAPH_SYNC", "0") == "1"  # diagnostics
+
+
+class GraphedStep:
+    def __init__(self, fn: Callable[[], Any], warmup: int = 3, enabled: bool = True):
+        """fn: the per-iteration device work.  It must read its inputs from tensors whose
+        storage stays the same between calls (copy new batches into them) and may return
+        tensors (or a structure of them); the returned objects are the graph's static outputs,
+        overwritten by every replay.  warmup: eager calls before capturing (autograd and the
+        allocator need them; they run on a side stream as capture requires)."""
+        self.fn = fn
+        self.warmup = max(1, int(warmup))
+        self.enabled = enabled
+        self.calls = 0
+        self.graph = None
+        self.out: Optional[Any] = None
+        self._side = None
+
+    @property
+    def captured(self) -> bool:
+        return self.graph is not None
+
+    def __call__(self) -> Any:
+        import torch
+
+        self.calls += 1
+        if not self.enabled or not torch.cuda.is_available():
+            return self.fn()
+        if self.graph is not None:
+            if _SYNC_BEFORE_REPLAY:
+                torch.cuda.synchronize()
+            self.graph.replay()
+            return self.out
+        cur = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        self._side.wait_stream(cur)
+        if self.calls <= self.warmup:
+            with torch.cuda.stream(self._side):
+                out = self.fn()
+            cur.wait_stream(self._side)
+            return out
+        return self._capture(cur)
+
+    def _capture(self, cur) -> Any:
+        import torch
+
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self._side):
+            self.out = self.fn()
+        self.graph = g
+        # capturing recorded the kernels without running them: this call's work is the replay
+        g.replay()
+        return self.out
