@@ -66,3 +66,41 @@ def test_error_mode_raises(native_build):
             rabit.allreduce(np.ones(2), rabit.BITOR)
     finally:
         rabit.finalize()
+
+
+FUZZ = os.path.join(ROOT, "tests", "scripts", "fuzz_collectives.py")
+FUZZ_PARAMS = {
+    "default": [],
+    "ring_small_buffer": ["rabit_reduce_ring_mincount=1", "rabit_reduce_buffer=4K"],
+    "tree_pipelined": ["rabit_reduce_ring_mincount=1000000", "rabit_tree_reduce_minsize=1K",
+                       "rabit_reduce_buffer=8K"],
+    "shm_chunked": ["rabit_host_shm_min=1K", "rabit_host_shm_buffer=64K"],
+    "tcp_only_no_elide": ["rabit_host_shm=0", "rabit_elide_consensus=0"],
+}
+
+
+@pytest.mark.parametrize("n", [2, 5])
+@pytest.mark.parametrize("name", sorted(FUZZ_PARAMS))
+def test_fuzz_collectives(native_build, name, n):
+    """Random allreduce (4 ops x 8 dtypes), broadcast (random roots) and variable, wrapping
+    allgather slices, sizes 0..300001 elements, exact against numpy, on every host algorithm
+    (ring / pipelined tree / shared memory, buffers smaller than the messages)."""
+    seed = 1000 + 17 * n + len(name)
+    job = LocalJob([sys.executable, FUZZ, str(seed), "60"] + FUZZ_PARAMS[name], n, 1,
+                   capture=True, timeout=180, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-3000:]
+    assert out.count("FUZZ OK") == n, out[-3000:]
+
+
+def test_fuzz_collectives_with_failures(native_build):
+    """The same random stream with three workers killed at different points (mock engine):
+    restarted workers resume from the last checkpoint and replay, every result stays exact."""
+    job = LocalJob([sys.executable, FUZZ, "5", "80", "lib=mock", "mock=1,2,3,0", "mock=3,4,0,0",
+                    "mock=0,4,7,0"], 4, 3, capture=True, timeout=240, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-3000:]
+    assert out.count("FUZZ OK") == 4, out[-3000:]
+    assert sum(a - 1 for a in job.attempts) == 3, job.attempts
