@@ -23,7 +23,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import rabit_amd as rabit  # noqa: E402
 from rabit_amd.parallel.data_parallel import GradientBuckets, shard  # noqa: E402
-from rabit_amd.parallel.graphs import GraphedStep  # noqa: E402
+from rabit_amd.parallel.graphs import GraphedStep, graph_safe_linear  # noqa: E402
 
 
 def main():
@@ -37,6 +37,11 @@ def main():
     ap.add_argument("--graph", type=int, default=0,
                     help="replay forward+backward as one hipGraph (GraphedStep); bit-identical")
     ap.add_argument("--layers", type=int, default=1, help="hidden layers of the MLP")
+    ap.add_argument("--bias", type=int, default=1, help="0: bias-free hidden layers")
+    ap.add_argument("--safe-linear", type=int, default=0,
+                    help="bias gradients as GEMVs (graph_safe_linear); use with --graph")
+    ap.add_argument("--trace-steps", type=int, default=0,
+                    help="print a digest of the local and the reduced gradients every step")
     args, rest = ap.parse_known_args()
     lib = "standard"
     params = []
@@ -62,10 +67,13 @@ def main():
     lo, hi = shard(args.rows, rank, world)
     xs, ys = X[lo:hi].to(dev), y[lo:hi].to(dev)
     torch.manual_seed(0)
-    layers = [torch.nn.Linear(d_in, args.hidden), torch.nn.Tanh()]
+    bias = bool(args.bias)
+    layers = [torch.nn.Linear(d_in, args.hidden, bias=bias), torch.nn.Tanh()]
     for _ in range(args.layers - 1):
-        layers += [torch.nn.Linear(args.hidden, args.hidden), torch.nn.Tanh()]
+        layers += [torch.nn.Linear(args.hidden, args.hidden, bias=bias), torch.nn.Tanh()]
     model = torch.nn.Sequential(*layers, torch.nn.Linear(args.hidden, 1)).to(dev)
+    if args.safe_linear:
+        graph_safe_linear(model)
     buckets = GradientBuckets(model.parameters(), bucket_mb=args.bucket_mb)
     flat = {"p%d" % i: p.data for i, p in enumerate(model.parameters())}
 
@@ -96,7 +104,17 @@ def main():
     step_fn = GraphedStep(compute) if (args.graph and dev.type == "cuda") else compute
     for step in range(start, args.steps):
         loss = step_fn()
-        buckets.reduce()  # average over ranks; replayed from the survivors' logs after a restart
+        if args.trace_steps:
+            local = [hashlib.sha1(b.detach().cpu().numpy().tobytes()).hexdigest()[:8]
+                     for b in buckets.buckets]
+        buckets.reduce()
+        if args.trace_steps:
+            red = [hashlib.sha1(b.detach().cpu().numpy().tobytes()).hexdigest()[:8]
+                   for b in buckets.buckets]
+            wts = hashlib.sha1(b"".join(p.detach().cpu().numpy().tobytes()
+                                        for p in model.parameters())).hexdigest()[:8]
+            print("[%d] TRACE step %d weights %s local %s reduced %s" % (
+                rank, step, wts, ",".join(local), ",".join(red)), flush=True)  # average over ranks; replayed from the survivors' logs after a restart
         with torch.no_grad():
             for p in model.parameters():
                 p.add_(p.grad, alpha=-args.lr)

@@ -11,4 +11,4 @@ GraphedStep       replays the launch-bound device part of an iteration (forward,
                   bucket zeroing) as one hipGraph; the collectives stay outside it.
 """
 from .data_parallel import FaultTolerantLoop, GradientBuckets  # noqa: F401
-from .graphs import GraphedStep  # noqa: F401
+from .graphs import GraphedStep, graph_safe_linear  # noqa: F401

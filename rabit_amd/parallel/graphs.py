@@ -34,10 +34,10 @@ captured *accumulating* backward pass replays exactly once and then yields wrong
 some shapes; the culprit is the column reduction of the bias gradient (torch.sum(x, 0) on
 [512, 1024] replays wrongly from its second replay on: tools/graph_reduce_check.py).
 
-Known open issue: with a worker killed and restarted mid-training, graphed dp_train runs finish
-with weights that agree on every rank but differ from the clean run (eager runs with the same
-failures match it bit for bit: tools/graph_check.py).  Until that is understood, use eager
-steps where bit-exact recovery matters.
+With workers killed and restarted, graphed runs of models with `nn.Linear` biases could end
+with different weights: the column reduction again, on a survivor's replay after the recovery.
+`graph_safe_linear(model)` computes bias gradients as GEMVs; with it (or without biases) every
+failure case tried is bit-identical to the clean eager run (tools/graph_check.py).
 """
 from __future__ import annotations
 
@@ -101,3 +101,46 @@ class GraphedStep:
         # capturing recorded the kernels without running them: this call's work is the replay
         g.replay()
         return self.out
+
+
+def _linear_fn():
+    import torch
+
+    class _GraphSafeLinear(torch.autograd.Function):
+        """nn.Linear with the bias gradient as a GEMV (dY^T @ 1) instead of a column reduction"""
+
+        @staticmethod
+        def forward(ctx, x, w, b):
+            ctx.save_for_backward(x, w)
+            ctx.has_bias = b is not None
+            return torch.nn.functional.linear(x, w, b)
+
+        @staticmethod
+        def backward(ctx, gy):
+            x, w = ctx.saved_tensors
+            gy2 = gy.reshape(-1, gy.shape[-1])
+            x2 = x.reshape(-1, x.shape[-1])
+            gx = (gy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+            gw = gy2.t() @ x2
+            gb = None
+            if ctx.has_bias:
+                ones = torch.ones(gy2.shape[0], dtype=gy.dtype, device=gy.device)
+                gb = torch.mv(gy2.t(), ones)
+            return gx, gw, gb
+
+    return _GraphSafeLinear
+
+
+def graph_safe_linear(model):
+    """Make every nn.Linear of `model` compute its bias gradient with a GEMV instead of the
+    column reduction torch uses (which this PyTorch-ROCm build replays wrongly from a hipGraph
+    for some shapes, profiles/r1_graphs/).  Same forward; the weight and input gradients are the
+    same GEMMs.  Apply it to the eager and the graphed model alike when their results are
+    compared bit for bit (the bias gradient's summation order differs from torch's)."""
+    import torch
+
+    fn = _linear_fn()
+    for m in model.modules():
+        if isinstance(m, torch.nn.Linear):
+            m.forward = (lambda mod: (lambda x: fn.apply(x, mod.weight, mod.bias)))(m)
+    return model

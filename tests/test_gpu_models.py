@@ -52,16 +52,22 @@ def test_dp_train_on_hbm_with_failures(native_build):
 
 def test_dp_train_graphed_step_matches_eager(native_build):
     """GraphedStep: forward+backward replayed as one hipGraph, the bucket allreduce (3 ranks on
-    the direct transport) outside it: the final weights equal the eager run's bit for bit."""
+    the direct transport) outside it: the final weights equal the eager run's bit for bit, also
+    with two workers killed and restarted mid-training (restarted workers capture their own
+    graph).  graph_safe_linear keeps torch's column reduction out of the graph (profiles/r1_graphs)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from test_examples import run_dp_train
-    args = ["--hidden", "256", "--layers", "6", "--bucket-mb", "1"]
+    args = ["--hidden", "256", "--layers", "6", "--bucket-mb", "1", "--safe-linear", "1"]
     eager, _, _ = run_dp_train(3, 1, args)
     graphed, _, out = run_dp_train(3, 1, args + ["--graph", "1"])
     assert out.count("graphed=1") == 3, out[-3000:]
     assert graphed == eager, (eager, graphed)
+    failed, job, out = run_dp_train(3, 3, args + ["--graph", "1", "mock=1,2,1,0",
+                                                  "mock=2,3,0,0"])
+    assert sum(a - 1 for a in job.attempts) >= 2, "kill points did not fire"
+    assert failed == eager, (eager, failed)
 
 
 def test_graphed_step_replays_exactly():

@@ -17,7 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import rabit_amd as rabit  # noqa: E402
-from rabit_amd.parallel import GradientBuckets, GraphedStep  # noqa: E402
+from rabit_amd.parallel import GradientBuckets, GraphedStep, graph_safe_linear  # noqa: E402
 
 
 def build(args, dev):
@@ -26,6 +26,8 @@ def build(args, dev):
     for _ in range(args.layers):
         layers += [torch.nn.Linear(args.hidden, args.hidden), torch.nn.Tanh()]
     model = torch.nn.Sequential(*layers, torch.nn.Linear(args.hidden, 1)).to(dev)
+    if args.safe_linear:
+        graph_safe_linear(model)
     buckets = GradientBuckets(model.parameters(), bucket_mb=256)
     return model, buckets
 
@@ -60,6 +62,7 @@ def run(args, dev, graphed):
         loss = step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    loss = float(loss.item())  # a graph's output is overwritten by the next replay
     # the pure GPU time of one step (one replayed graph + collective), from device events
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
@@ -69,7 +72,7 @@ def run(args, dev, graphed):
     torch.cuda.synchronize()
     w = torch.cat([p.detach().reshape(-1) for p in params])
     info = {"captured": bool(getattr(step_fn, "captured", False))}
-    return dt, ev0.elapsed_time(ev1) / args.steps * 1e-3, float(loss.item()), w, info
+    return dt, ev0.elapsed_time(ev1) / args.steps * 1e-3, loss, w, info
 
 
 def main():
@@ -79,12 +82,14 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--safe-linear", type=int, default=0,
+                    help="bias gradients as GEMVs in both runs (graph_safe_linear)")
     args = ap.parse_args()
     rabit.init([], lib="standard", rabit_world1_fastpath=0)
     dev = torch.device("cuda", 0)
     t_eager, g_eager, l_eager, w_eager, _ = run(args, dev, False)
     t_graph, g_graph, l_graph, w_graph, info = run(args, dev, True)
-    rec = {"probe": "graphed_step", "layers": args.layers, "hidden": args.hidden,
+    rec = {"probe": "graphed_step", "safe_linear": args.safe_linear, "layers": args.layers, "hidden": args.hidden,
            "batch": args.batch, "steps": args.steps,
            "eager_us": round(t_eager * 1e6, 1), "graphed_us": round(t_graph * 1e6, 1),
            "speedup": round(t_eager / t_graph, 2),
