@@ -34,10 +34,13 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
  *        alignment check and must be aligned like the table's pointers).  post_scale != 0
  *        multiplies the reduced value (float/double only): the averaging of a data-parallel
  *        gradient applied once after the sum, so the inputs can be read unmodified.
+ *        dst2: optional second destination written with the same values by the same kernel
+ *        (the user buffer next to the result log: one launch and one read instead of two).
  */
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard = nullptr,
-                             const void *const *table = nullptr, double post_scale = 0.0);
+                             const void *const *table = nullptr, double post_scale = 0.0,
+                             void *dst2 = nullptr);
 /*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);

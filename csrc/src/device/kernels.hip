@@ -178,6 +178,7 @@ struct SrcList {
   const int *guard;  // optional: skip the whole launch when *guard != 0 (failed peer barrier)
   const void *const *table;  // optional: device table of source pointers (overrides p)
   double post_scale;         // != 0: multiply the reduced value by it (floating types)
+  void *dst2;                // optional second destination (same values as dst)
 };
 
 /*! \brief source k: from the device table when given (written by an earlier kernel, e.g. a
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
   const size_t nvec = n * sizeof(T) / 16;
   const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * U + threadIdx.x;
   uint4 *d = reinterpret_cast<uint4 *>(dst);
+  uint4 *d2 = reinterpret_cast<uint4 *>(srcs.dst2);
   if (base + (U - 1) * kBlock < nvec) {
     uint4 x[NSRC][U];
 #pragma unroll
@@ -211,6 +213,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, x[k][u]);
       if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
       StoreNT(d + base + u * kBlock, acc);
+      if (d2 != nullptr) StoreNT(d2 + base + u * kBlock, acc);
     }
   } else {
     for (int u = 0; u < U; ++u) {
@@ -222,6 +225,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       }
       if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
       StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
+      if (d2 != nullptr) StoreNT(d2 + i, acc);
     }
   }
   Tail<T>(nvec, n, [&](size_t i) {
@@ -230,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
     if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
     dst[i] = acc;
+    if (srcs.dst2 != nullptr) static_cast<T *>(srcs.dst2)[i] = acc;
   });
 }
 
@@ -242,6 +247,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcLis
   for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
   if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
   dst[i] = acc;
+  if (srcs.dst2 != nullptr) static_cast<T *>(srcs.dst2)[i] = acc;
 }
 
 template <typename T, int OP, int NSRC>
@@ -254,12 +260,14 @@ void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
 
 template <typename T, int OP>
 hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st,
-                       const int *guard, const void *const *table, double post_scale) {
+                       const int *guard, const void *const *table, double post_scale,
+                       void *dst2) {
   SrcList sl;
   sl.guard = guard;
   sl.table = table;
   sl.post_scale = post_scale;
-  bool aligned = Aligned16(dst);
+  sl.dst2 = dst2;
+  bool aligned = Aligned16(dst) && (dst2 == nullptr || Aligned16(dst2));
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;
     if (k < nsrc) aligned = aligned && Aligned16(srcs[k]);
@@ -482,9 +490,9 @@ struct OrTag {
     return hipErrorInvalidValue;
   }
   static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st,
-                            const int *guard, const void *const *table) {
+                            const int *guard, const void *const *table, void *d2) {
     if constexpr (std::is_integral<T>::value) {
-      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table, 0.0);
+      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table, 0.0, d2);
     }
     return hipErrorInvalidValue;
   }
@@ -508,17 +516,20 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard,
-                             const void *const *table, double post_scale) {
+                             const void *const *table, double post_scale, void *dst2) {
   if (count == 0) return hipSuccess;
   if (post_scale != 0.0 && dtype != 6 && dtype != 7) return hipErrorInvalidValue;  // float/double
   if (nsrc < 1 || nsrc > kMaxReduceSources) return hipErrorInvalidValue;
   return DispatchType(dtype, op == kOpOr, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;
     switch (op) {
-      case kOpMax: return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
-      case kOpMin: return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
-      case kOpSum: return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table, post_scale);
-      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table);
+      case kOpMax:
+        return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
+      case kOpMin:
+        return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
+      case kOpSum:
+        return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
+      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table, dst2);
       default: return hipErrorInvalidValue;
     }
   });

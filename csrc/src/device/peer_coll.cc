@@ -206,7 +206,7 @@ hipError_t PeerGroup::Allreduce(const void *send, void *recv, void *recv2, size_
     return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table, post);
   };
   return AllreduceImpl(send, recv, recv2, count, ElemBytes(dtype), dtype, prep, alpha, step,
-                       true, op == 2);
+                       true, op == 2, op);
 }
 
 hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
@@ -217,7 +217,8 @@ hipError_t PeerGroup::AllreduceCustom(const void *send, void *recv, void *recv2,
 
 hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, size_t count,
                                     size_t tn, int dtype, int prep, double alpha,
-                                    const ReduceStep &step, bool indirect, bool op_is_sum) {
+                                    const ReduceStep &step, bool indirect, bool op_is_sum,
+                                    int builtin_op) {
   utils::Assert(opened_, "peer group not opened");
   // segments are multiples of 256 elements: 256-byte aligned for any element size
   const size_t quantum = 256 * static_cast<size_t>(n_);
@@ -286,11 +287,18 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       XRABIT_TRY_HIP(mark(2));
       const void *srcs[kMaxPeers];
       for (int p = 0; p < n_; ++p) srcs[p] = stage(p, which);
-      XRABIT_TRY_HIP(step(out + off * tn, srcs, n_, c, dev_status(), table_,
-                          post_scale ? alpha : 0.0, stream_));
+      if (builtin_op >= 0) {
+        // built-in op: the same kernel also stores the result into the second destination
+        XRABIT_TRY_HIP(LaunchReduceMulti(out + off * tn, srcs, n_, c, dtype, builtin_op, stream_,
+                                         dev_status(), table_, post_scale ? alpha : 0.0,
+                                         out2 != nullptr ? out2 + off * tn : nullptr));
+      } else {
+        XRABIT_TRY_HIP(step(out + off * tn, srcs, n_, c, dev_status(), table_,
+                            post_scale ? alpha : 0.0, stream_));
+      }
       XRABIT_TRY_HIP(mark(3));
       XRABIT_TRY_HIP(mark(4));  // (no second barrier)
-      if (out2 != nullptr) {
+      if (out2 != nullptr && builtin_op < 0) {
         CopyBatch b;
         NewBatch(&b);
         AddSeg(&b, out2 + off * tn, out + off * tn, nullptr, c * tn);

@@ -181,7 +181,7 @@ class PeerGroup {
   hipError_t Barrier(const ResolveArgs *resolve = nullptr);
   hipError_t AllreduceImpl(const void *send, void *recv, void *recv2, size_t count, size_t tn,
                            int dtype, int prep, double alpha, const ReduceStep &step,
-                           bool indirect, bool op_is_sum = false);
+                           bool indirect, bool op_is_sum = false, int builtin_op = -1);
   /*! \brief true if [p, p + bytes) lies in this rank's symmetric heap */
   bool InHeap(const void *p, size_t bytes) const {
     const char *c = static_cast<const char *>(p);
