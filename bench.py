@@ -158,7 +158,9 @@ def main():
     n = args.size_mb * (1 << 20) // 4
     if args.symmetric < 0:
         args.symmetric = 1 if world > 1 else 0
-    heap = {"rabit_device_symmetric_heap": str(n * 4 + (16 << 20))} if args.symmetric else {}
+    # + 48 MiB: the calibration's 32 MiB inputs come from the heap's free tail, so it times the
+    # paths heap buffers take
+    heap = {"rabit_device_symmetric_heap": str(n * 4 + (48 << 20))} if args.symmetric else {}
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
                         rabit_world1_fastpath=0, rabit_device=gpu, **heap)
     dev = torch.device("cuda", gpu)
@@ -235,7 +237,8 @@ def main():
                       "direct_min_bytes": st.get("device_direct_min", -1),
                       "calibration_us": st.get("calib_us"),
                       "direct_variant": "push" if st.get("direct_push") else "pull",
-                      "calibration_push_us": st.get("calib_push_us")},
+                      "calibration_push_us": st.get("calib_push_us"),
+                      "calibration_heap_inputs": bool(st.get("calib_heap_src", 0))},
         "extras": extras,
         "reference_measured": reference_measured(world, aggregate),
     }

@@ -388,7 +388,14 @@ Status EngineBase::CalibrateDevice() {
   // sizes in float32 elements; every rank runs the same sequence (this is a collective)
   const size_t big = std::min<size_t>(32u << 20, dev_->has_peers() ? dcfg_.peer_stage : 0) / 4;
   const size_t sizes[2] = {64u << 10, std::max<size_t>(big, 1u << 20)};
-  float *src = static_cast<float *>(dev_->Scratch(sizes[1] * 4, 0));
+  // Inputs come from the free tail of the symmetric heap when the job has one: its buffers
+  // live there, and the calibration then times the paths they take (the direct transport reads
+  // heap inputs in place; RCCL reads the same uncached memory).  Otherwise from scratch HBM.
+  const device::SymHeapInfo &heap = dev_->sym_heap();
+  const bool heap_src =
+      heap.base != nullptr && heap.bytes - dev_->sym_heap_used() >= sizes[1] * 4;
+  float *src = heap_src ? reinterpret_cast<float *>(heap.base + dev_->sym_heap_used())
+                        : static_cast<float *>(dev_->Scratch(sizes[1] * 4, 0));
   float *dst = static_cast<float *>(dev_->Scratch(sizes[1] * 4, 1));
   const int n = GetWorldSize();
   double t[2][2] = {{0, 0}, {0, 0}};  // [transport: 0 rccl, 1 direct][size]
@@ -502,6 +509,7 @@ Status EngineBase::CalibrateDevice() {
   }
   calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
             static_cast<double>(sizes[1] * 4), agg[4]};
+  calib_heap_src_ = heap_src;
   if (debug_ || rank_ == 0) {
     utils::HandleLogInfo(
         "[xrabit] device calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B rccl "
@@ -810,6 +818,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
      << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
      << ",\"calib_push_us\":" << calib_.push_big * 1e6
+     << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0);
   double phase[device::PeerGroup::kPhases];

@@ -192,6 +192,7 @@ class EngineBase : public IEngine {
   struct {
     double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes, push_big;
   } calib_{0, 0, 0, 0, 0, 0, 0};
+  bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
   bool trace_spans_{false};
   bool trace_roctx_{false};
   size_t trace_capacity_{1 << 16};

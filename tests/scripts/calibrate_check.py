@@ -26,5 +26,8 @@ assert lo == hi, (lo, hi)
 assert st["calib_push_us"] > 0, st
 push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
 assert push in (0, world), push
+# with a symmetric heap that has room, the calibration reads its inputs from the heap's tail
+want_heap = any(a.startswith("rabit_device_symmetric_heap=") for a in sys.argv[1:])
+assert st["calib_heap_src"] == (1 if want_heap else 0), st
 rabit.finalize()
 print("[%d] CALIB OK thr=%s calib=%s" % (rank, thr, calib), flush=True)

@@ -65,10 +65,11 @@ def test_host_buffers_via_device():
     assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
 
 
-def test_calibration_flow():
+@pytest.mark.parametrize("extra", [[], ["rabit_device_symmetric_heap=64M"]])
+def test_calibration_flow(extra):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("calibrate_check.py", 3)
+    rc, out = _run("calibrate_check.py", 3, extra)
     assert rc == 0, out[-5000:]
     assert out.count("CALIB OK") == 3, out[-3000:]
 
