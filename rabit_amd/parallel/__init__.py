@@ -9,6 +9,9 @@ FaultTolerantLoop resume-from-checkpoint training loop (LoadCheckPoint / CheckPo
                   k steps), the rabit programming model for iterative jobs.
 GraphedStep       replays the launch-bound device part of an iteration (forward, backward,
                   bucket zeroing) as one hipGraph; the collectives stay outside it.
+CommThread,       the engine on its own host thread; bucket allreduces start from backward
+OverlappedBuckets hooks and run on their own HIP stream while backward continues.
 """
 from .data_parallel import FaultTolerantLoop, GradientBuckets  # noqa: F401
 from .graphs import GraphedStep, graph_safe_linear  # noqa: F401
+from .overlap import CommThread, OverlappedBuckets  # noqa: F401

@@ -98,3 +98,30 @@ def test_graphed_step_replays_exactly():
         torch.cuda.synchronize()
         assert all(torch.equal(a, b) for a, b in zip(grads, ref))
     assert step.captured
+
+
+def test_overlapped_buckets_on_device(native_build):
+    """OverlappedBuckets on HBM (3 ranks on the box's GPU, direct transport): bucket
+    allreduces run on the comm thread's HIP stream during backward; the weights equal those
+    of reducing after backward, also with a worker killed and restarted."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import re
+    script = os.path.join(ROOT, "tests", "scripts", "overlap_check.py")
+
+    def run(mode, extra=(), attempts=1):
+        job = LocalJob([sys.executable, script, mode, "10", "gpu"] + list(extra), 3, attempts,
+                       capture=True, timeout=240, print_fn=lambda m: None)
+        rc = job.run()
+        out = "".join("".join(o) for o in job.outputs)
+        assert rc == 0, out[-4000:]
+        d = set(re.findall(r"weights=([0-9a-f]+)", out))
+        assert len(d) == 1 and out.count("OVERLAP OK") == 3, out[-3000:]
+        return d.pop(), job
+
+    seq, _ = run("seq")
+    ovl, _ = run("overlap")
+    assert ovl == seq
+    failed, job = run("overlap", ["lib=mock", "mock=1,1,3,0"], attempts=3)
+    assert sum(a - 1 for a in job.attempts) == 1, job.attempts
+    assert failed == seq

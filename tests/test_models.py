@@ -1,5 +1,6 @@
 """Model families over several CPU ranks, with and without injected failures."""
 import os
+import re
 import sys
 
 import pytest
@@ -34,3 +35,29 @@ def test_model_survives_failures(native_build, which, mock):
     assert rc == 0, out[-3000:]
     assert out.count("MODEL OK") == 3
     assert sum(a - 1 for a in job.attempts) >= 1, "kill point not reached"
+
+
+OVERLAP = os.path.join(ROOT, "tests", "scripts", "overlap_check.py")
+
+
+def _overlap_job(mode, where, extra=(), n=3, attempts=1):
+    job = LocalJob([sys.executable, OVERLAP, mode, "12", where] + list(extra), n, attempts,
+                   capture=True, timeout=240, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-4000:]
+    digests = set(re.findall(r"OVERLAP OK mode=\w+ weights=([0-9a-f]+)", out))
+    assert len(digests) == 1 and out.count("OVERLAP OK") == n, out[-3000:]
+    return digests.pop(), job
+
+
+def test_overlapped_buckets_match_sequential(native_build):
+    """CommThread + OverlappedBuckets (allreduces started from backward hooks on the comm
+    thread) train to the same weights as reducing after backward, also with workers killed."""
+    seq, _ = _overlap_job("seq", "cpu")
+    ovl, _ = _overlap_job("overlap", "cpu")
+    assert ovl == seq
+    failed, job = _overlap_job("overlap", "cpu", ["lib=mock", "mock=1,1,2,0", "mock=2,2,0,0"],
+                               attempts=3)
+    assert sum(a - 1 for a in job.attempts) == 2, job.attempts
+    assert failed == seq
