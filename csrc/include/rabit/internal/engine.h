@@ -57,8 +57,15 @@ enum DataType {
   kFloat = 6,
   kDouble = 7,
   kLongLong = 8,
-  kULongLong = 9
+  kULongLong = 9,
+  // extensions (no reference equivalent): 16-bit floats, rabit/internal/half.h
+  kHalf = 10,
+  kBFloat16 = 11
 };
+/*! \brief floating-point dtypes (BitOR is undefined for them) */
+inline bool IsFloating(int d) {
+  return d == kFloat || d == kDouble || d == kHalf || d == kBFloat16;
+}
 }  // namespace mpi
 
 /*! \brief interface of an Allreduce engine */

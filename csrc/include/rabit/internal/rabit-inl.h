@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "rabit/internal/engine.h"
+#include "rabit/internal/half.h"
 #include "rabit/internal/io.h"
 #include "rabit/internal/utils.h"
 
@@ -33,6 +34,8 @@ template <> inline DataType GetType<float>() { return kFloat; }
 template <> inline DataType GetType<double>() { return kDouble; }
 template <> inline DataType GetType<long long>() { return kLongLong; }            // NOLINT(*)
 template <> inline DataType GetType<unsigned long long>() { return kULongLong; }  // NOLINT(*)
+template <> inline DataType GetType<half_t>() { return kHalf; }
+template <> inline DataType GetType<bf16_t>() { return kBFloat16; }
 }  // namespace mpi
 }  // namespace engine
 

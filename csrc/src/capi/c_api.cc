@@ -84,7 +84,7 @@ struct BlobReader : public rabit::Serializable {
 };
 
 rabit::engine::mpi::DataType ToDType(int d) {
-  rabit::utils::Check(d >= 0 && d <= 9, "unknown dtype enum %d", d);
+  rabit::utils::Check(d >= 0 && d <= 11, "unknown dtype enum %d", d);
   return static_cast<rabit::engine::mpi::DataType>(d);
 }
 rabit::engine::mpi::OpType ToOp(int o) {
@@ -146,8 +146,7 @@ RABIT_DLL void RabitAllreduce(void *sendrecvbuf, size_t count, int enum_dtype, i
     const auto dtype = ToDType(enum_dtype);
     const auto op = ToOp(enum_op);
     if (op == rabit::engine::mpi::kBitwiseOR) {
-      rabit::utils::Check(dtype != rabit::engine::mpi::kFloat &&
-                              dtype != rabit::engine::mpi::kDouble,
+      rabit::utils::Check(!rabit::engine::mpi::IsFloating(dtype),
                           "BitOR is not defined for floating point types");
     }
     rabit::engine::ReduceFn red = rabit::coll::HostReducer(dtype, op);

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "rabit/internal/half.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -62,6 +63,8 @@ ReduceFn HostReducer(DataType dtype, OpType op) {
     case engine::mpi::kDouble: return PickOp<double>(op);
     case engine::mpi::kLongLong: return PickOp<int64_t>(op);
     case engine::mpi::kULongLong: return PickOp<uint64_t>(op);
+    case engine::mpi::kHalf: return PickOp<half_t>(op);
+    case engine::mpi::kBFloat16: return PickOp<bf16_t>(op);
   }
   return nullptr;
 }
@@ -70,6 +73,8 @@ size_t DTypeSize(DataType dtype) {
   switch (dtype) {
     case engine::mpi::kChar:
     case engine::mpi::kUChar: return 1;
+    case engine::mpi::kHalf:
+    case engine::mpi::kBFloat16: return 2;
     case engine::mpi::kInt:
     case engine::mpi::kUInt:
     case engine::mpi::kFloat: return 4;

@@ -40,6 +40,8 @@ bool RcclType(int dtype, ncclDataType_t *out) {
     case 7: *out = ncclFloat64; return true;
     case 8: *out = ncclInt64; return true;
     case 9: *out = ncclUint64; return true;
+    case 10: *out = ncclFloat16; return true;
+    case 11: *out = ncclBfloat16; return true;
     default: return false;
   }
 }
@@ -57,6 +59,8 @@ size_t TypeBytes(int dtype) {
   switch (dtype) {
     case 0:
     case 1: return 1;
+    case 10:
+    case 11: return 2;
     case 2:
     case 3:
     case 6: return 4;

@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "device/kernels.h"
+#include "rabit/internal/half.h"
 
 namespace rabit {
 namespace device {
@@ -154,7 +155,9 @@ __device__ __forceinline__ T PrepApply(T x, int prep, T alpha) {
     case kPrepSquare: return x * x;
     case kPrepScale: return x * alpha;
     case kPrepAbs:
-      if constexpr (std::is_signed<T>::value) return x < T(0) ? T(0) - x : x;
+      if constexpr (std::is_signed<T>::value || IsHalfType<T>::value) {
+        return x < T(0) ? T(0) - x : x;
+      }
       return x;
     default: return x;
   }
@@ -192,6 +195,56 @@ __device__ __forceinline__ bool Guarded(const int *guard) {
          __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
 
+/*! \brief op over NSRC 16-byte vectors, then the optional post scale.  16-bit floats are
+ *  widened: every element is accumulated over all sources in fp32 and rounded once */
+template <typename T, int OP, int NSRC>
+__device__ __forceinline__ uint4 ReduceVecs(const uint4 *v, double post) {
+  if constexpr (IsHalfType<T>::value) {
+    constexpr int L = 8;
+    T t[L];
+    float acc[L];
+    __builtin_memcpy(t, &v[0], 16);
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = t[j].f();
+#pragma unroll
+    for (int k = 1; k < NSRC; ++k) {
+      __builtin_memcpy(t, &v[k], 16);
+#pragma unroll
+      for (int j = 0; j < L; ++j) acc[j] = Apply<float, OP>::f(acc[j], t[j].f());
+    }
+    const float ps = static_cast<float>(post);
+#pragma unroll
+    for (int j = 0; j < L; ++j) t[j] = T(post != 0.0 ? acc[j] * ps : acc[j]);
+    uint4 r;
+    __builtin_memcpy(&r, t, 16);
+    return r;
+  } else {
+    uint4 acc = v[0];
+#pragma unroll
+    for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, v[k]);
+    if (post != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(post));
+    return acc;
+  }
+}
+
+/*! \brief scalar form of ReduceVecs over nsrc sources (tails, unaligned buffers) */
+template <typename T, int OP>
+__device__ __forceinline__ T ReduceScalar(const SrcList &srcs, int nsrc, size_t i) {
+  if constexpr (IsHalfType<T>::value) {
+    float acc = static_cast<const T *>(Src(srcs, 0))[i].f();
+    for (int k = 1; k < nsrc; ++k) {
+      acc = Apply<float, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i].f());
+    }
+    if (srcs.post_scale != 0.0) acc *= static_cast<float>(srcs.post_scale);
+    return T(acc);
+  } else {
+    T acc = static_cast<const T *>(Src(srcs, 0))[i];
+    for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
+    if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
+    return acc;
+  }
+}
+
 template <typename T, int OP, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList srcs, size_t n) {
   if (Guarded(srcs.guard)) return;
@@ -208,10 +261,10 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      uint4 acc = x[0][u];
+      uint4 v[NSRC];
 #pragma unroll
-      for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, x[k][u]);
-      if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
+      for (int k = 0; k < NSRC; ++k) v[k] = x[k][u];
+      const uint4 acc = ReduceVecs<T, OP, NSRC>(v, srcs.post_scale);
       StoreNT(d + base + u * kBlock, acc);
       if (d2 != nullptr) StoreNT(d2 + base + u * kBlock, acc);
     }
@@ -219,20 +272,16 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     for (int u = 0; u < U; ++u) {
       const size_t i = base + u * kBlock;
       if (i >= nvec) break;
-      uint4 acc = reinterpret_cast<const uint4 *>(Src(srcs, 0))[i];
-      for (int k = 1; k < NSRC; ++k) {
-        acc = Combine<T, OP>(acc, reinterpret_cast<const uint4 *>(Src(srcs, k))[i]);
-      }
-      if (srcs.post_scale != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(srcs.post_scale));
+      uint4 v[NSRC];
+#pragma unroll
+      for (int k = 0; k < NSRC; ++k) v[k] = reinterpret_cast<const uint4 *>(Src(srcs, k))[i];
+      const uint4 acc = ReduceVecs<T, OP, NSRC>(v, srcs.post_scale);
       StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
       if (d2 != nullptr) StoreNT(d2 + i, acc);
     }
   }
   Tail<T>(nvec, n, [&](size_t i) {
-    T acc = static_cast<const T *>(Src(srcs, 0))[i];
-#pragma unroll
-    for (int k = 1; k < NSRC; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
-    if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
+    const T acc = ReduceScalar<T, OP>(srcs, NSRC, i);
     dst[i] = acc;
     if (srcs.dst2 != nullptr) static_cast<T *>(srcs.dst2)[i] = acc;
   });
@@ -243,9 +292,7 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiScalarKernel(T *dst, SrcLis
                                                                   size_t n) {
   const size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n || Guarded(srcs.guard)) return;
-  T acc = static_cast<const T *>(Src(srcs, 0))[i];
-  for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
-  if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
+  const T acc = ReduceScalar<T, OP>(srcs, nsrc, i);
   dst[i] = acc;
   if (srcs.dst2 != nullptr) static_cast<T *>(srcs.dst2)[i] = acc;
 }
@@ -478,6 +525,8 @@ hipError_t DispatchType(int dtype, bool int_only, Fn &&fn) {
     case 7: return int_only ? hipErrorInvalidValue : fn(static_cast<double *>(nullptr));
     case 8: return fn(static_cast<int64_t *>(nullptr));
     case 9: return fn(static_cast<uint64_t *>(nullptr));
+    case 10: return int_only ? hipErrorInvalidValue : fn(static_cast<half_t *>(nullptr));
+    case 11: return int_only ? hipErrorInvalidValue : fn(static_cast<bf16_t *>(nullptr));
     default: return hipErrorInvalidValue;
   }
 }
@@ -518,7 +567,9 @@ hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_
                              int dtype, int op, hipStream_t stream, const int *guard,
                              const void *const *table, double post_scale, void *dst2) {
   if (count == 0) return hipSuccess;
-  if (post_scale != 0.0 && dtype != 6 && dtype != 7) return hipErrorInvalidValue;  // float/double
+  if (post_scale != 0.0 && dtype != 6 && dtype != 7 && dtype != 10 && dtype != 11) {
+    return hipErrorInvalidValue;  // floating types only
+  }
   if (nsrc < 1 || nsrc > kMaxReduceSources) return hipErrorInvalidValue;
   return DispatchType(dtype, op == kOpOr, [&](auto *tag) -> hipError_t {
     using T = typename std::remove_pointer<decltype(tag)>::type;

@@ -20,6 +20,8 @@ size_t ElemBytes(int dtype) {
   switch (dtype) {
     case 0:
     case 1: return 1;
+    case 10:
+    case 11: return 2;
     case 2:
     case 3:
     case 6: return 4;
@@ -230,7 +232,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   char *out2 = static_cast<char *>(recv2);
   // sum(a x_p) = a sum(x_p): exact reordering only for the linear op
   const bool post_scale =
-      indirect && op_is_sum && prep == kPrepScale && (dtype == 6 || dtype == 7);
+      indirect && op_is_sum && prep == kPrepScale &&
+      (dtype == 6 || dtype == 7 || dtype == 10 || dtype == 11);
   const int stage_prep = post_scale ? kPrepCopy : prep;
   // per-phase timing of single-chunk ops (rabit_device_phase_timing=1)
   const bool timed = timing_ && count <= chunk;

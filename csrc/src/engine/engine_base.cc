@@ -253,7 +253,7 @@ void EngineBase::ReportStatus() const {
 Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec, const void *src) {
   const size_t bytes = spec.bytes();
   if (host_via_device_ && dev_ && GetWorldSize() > 1 && spec.builtin() && bytes >= host_dev_min_ &&
-      !(spec.op == mpi::kBitwiseOR && (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble))) {
+      !(spec.op == mpi::kBitwiseOR && mpi::IsFloating(spec.dtype))) {
     // large host buffer on a GPU node: stage through HBM and use the device transports (the
     // role of the reference's MPI engine: vendor collectives instead of TCP)
     device::DeviceGuard dg(dev_->device());
@@ -529,9 +529,9 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   if (bytes == 0) return Status::kSuccess;
   if (dst2 == dst) dst2 = nullptr;
   device::DeviceGuard dg(dev_->device());
-  bool rccl_ok = spec.builtin() && spec.dtype <= mpi::kULongLong;
+  bool rccl_ok = spec.builtin() && spec.dtype <= mpi::kBFloat16;
   if (spec.builtin() && spec.op == mpi::kBitwiseOR &&
-      (spec.dtype == mpi::kFloat || spec.dtype == mpi::kDouble)) {
+      mpi::IsFloating(spec.dtype)) {
     utils::Error("BitOR is not defined for floating point types");
   }
   dev_->EnterFromUser();

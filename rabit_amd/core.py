@@ -45,6 +45,7 @@ DTYPE_ENUM = {
     np.dtype("uint64"): 5,
     np.dtype("float32"): 6,
     np.dtype("float64"): 7,
+    np.dtype("float16"): 10,  # extension: IEEE half (mpi::kHalf)
 }
 DTYPE_ENUM__ = DTYPE_ENUM  # reference spelling
 
@@ -53,7 +54,7 @@ def _torch_dtype_enum(t) -> int:
     import torch
 
     table = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float32: 6,
-             torch.float64: 7}
+             torch.float64: 7, torch.float16: 10, torch.bfloat16: 11}
     for name, code in (("uint32", 3), ("uint64", 5)):
         if hasattr(torch, name):
             table[getattr(torch, name)] = code
@@ -186,6 +187,8 @@ def allreduce(data, op: int, prepare_fun: Optional[Callable] = None):
     if _is_torch(data):
         if not data.is_contiguous():
             raise ValueError("allreduce needs a contiguous tensor")
+        if op == BITOR and data.is_floating_point():
+            raise TypeError("BITOR is not defined for floating point data")
         enum = _torch_dtype_enum(data)
         if data.is_cuda:
             _sync_stream_for(data)
@@ -421,10 +424,12 @@ def symmetric_empty(shape, dtype=None):
         raise MemoryError("symmetric heap unavailable or full (rabit_device_symmetric_heap)")
     typestr = {torch.float32: "<f4", torch.float64: "<f8", torch.int32: "<i4",
                torch.int64: "<i8", torch.uint8: "|u1", torch.int8: "|i1",
-               torch.float16: "<f2"}[dtype]
+               torch.float16: "<f2", torch.bfloat16: "<i2"}[dtype]
     dev = torch.device("cuda", get_device())
     with torch.cuda.device(dev):
         t = torch.as_tensor(_DeviceArray(ptr, shape, typestr, None), device=dev)
+    if dtype == torch.bfloat16:  # no array-interface code for bf16: same bits as int16
+        t = t.view(torch.bfloat16)
     assert t.data_ptr() == ptr, "torch copied the symmetric buffer"
     return t
 

@@ -30,7 +30,7 @@ def dtype_enum(t) -> int:
     import torch
 
     table = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float32: 6,
-             torch.float64: 7}
+             torch.float64: 7, torch.float16: 10, torch.bfloat16: 11}
     for name, code in (("uint32", 3), ("uint64", 5)):
         if hasattr(torch, name):
             table[getattr(torch, name)] = code

@@ -6,6 +6,7 @@
  * allreduce_mock_test, allreduce_robust_test) against xrabit internals, plus serializer,
  * reducer and consensus-encoding tests.  All tests run in single-node mode (no tracker).
  */
+#include <rabit/internal/half.h>
 #include <rabit/internal/io.h>
 #include <rabit/internal/utils.h>
 #include <rabit/rabit.h>
@@ -14,6 +15,7 @@
 #include <chrono>
 #include <cstdio>
 #include <functional>
+#include <limits>
 #include <map>
 #include <string>
 #include <thread>
@@ -318,6 +320,44 @@ TEST(robust_shutdown_before_timeout) {
   EXPECT(r.Shutdown());
   std::this_thread::sleep_for(std::chrono::milliseconds(1200));
   EXPECT(g_timeouts.load() == 0);
+}
+
+TEST(half_types_roundtrip_and_rounding) {
+  // every non-NaN binary16 / bfloat16 pattern survives f() -> FromFloat()
+  int bad = 0;
+  for (uint32_t b = 0; b < 65536; ++b) {
+    rabit::half_t h;
+    h.bits = static_cast<uint16_t>(b);
+    const float f = h.f();
+    if (f == f && rabit::half_t(f).bits != h.bits) ++bad;
+    rabit::bf16_t g;
+    g.bits = static_cast<uint16_t>(b);
+    const float fg = g.f();
+    if (fg == fg && rabit::bf16_t(fg).bits != g.bits) ++bad;
+  }
+  EXPECT(bad == 0);
+  EXPECT(rabit::half_t(1.0f).bits == 0x3c00);
+  EXPECT(rabit::half_t(65504.0f).bits == 0x7bff);
+  EXPECT(rabit::half_t(65520.0f).bits == 0x7c00);            // rounds to inf
+  EXPECT(rabit::half_t(5.9604645e-08f).bits == 0x0001);      // 2^-24, smallest subnormal
+  EXPECT(rabit::half_t(2.9802322e-08f).bits == 0x0000);      // 2^-25 ties to even (zero)
+  EXPECT(rabit::half_t(1.0f + 1.0f / 2048).bits == 0x3c00);  // tie -> even
+  EXPECT(rabit::half_t(1.0f + 3.0f / 2048).bits == 0x3c02);  // tie -> even (up)
+  EXPECT(rabit::bf16_t(1.0f).bits == 0x3f80);
+  EXPECT(rabit::bf16_t(1.0f + 1.0f / 256).bits == 0x3f80);   // tie -> even
+  EXPECT(rabit::bf16_t(1.0f + 3.0f / 256).bits == 0x3f82);
+  const float nan = std::numeric_limits<float>::quiet_NaN();
+  EXPECT(rabit::half_t(nan).f() != rabit::half_t(nan).f());
+  EXPECT(rabit::bf16_t(nan).f() != rabit::bf16_t(nan).f());
+  // the host reducer of the extended enum
+  rabit::bf16_t a[3] = {rabit::bf16_t(1.0f), rabit::bf16_t(-2.0f), rabit::bf16_t(3.5f)};
+  rabit::bf16_t b[3] = {rabit::bf16_t(2.0f), rabit::bf16_t(5.0f), rabit::bf16_t(-1.0f)};
+  rabit::coll::HostReducer(rabit::engine::mpi::kBFloat16, rabit::engine::mpi::kSum)(
+      b, a, 3, MPI::Datatype(2));
+  EXPECT(a[0].f() == 3.0f && a[1].f() == 3.0f && a[2].f() == 2.5f);
+  EXPECT(rabit::coll::HostReducer(rabit::engine::mpi::kHalf, rabit::engine::mpi::kBitwiseOR) ==
+         nullptr);
+  EXPECT(rabit::coll::DTypeSize(rabit::engine::mpi::kHalf) == 2);
 }
 
 TEST(wait_state_working_vs_waiting) {

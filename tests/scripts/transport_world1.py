@@ -17,7 +17,8 @@ rabit.init(sys.argv[2:], lib="standard", rabit_device=0, rabit_world1_fastpath=0
 assert rabit.get_world_size() == 1
 dev = torch.device("cuda", 0)
 checked = 0
-for dt in (torch.int8, torch.uint8, torch.int32, torch.int64, torch.float32, torch.float64):
+for dt in (torch.int8, torch.uint8, torch.int32, torch.int64, torch.float32, torch.float64,
+           torch.float16, torch.bfloat16):
     ops = [rabit.MAX, rabit.MIN, rabit.SUM] + ([rabit.BITOR] if not dt.is_floating_point else [])
     for op in ops:
         for n in (1, 1000, 65536 + 3, (3 << 20) // torch.tensor([], dtype=dt).element_size() + 5):

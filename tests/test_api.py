@@ -61,7 +61,7 @@ def test_error_mode_raises(native_build):
     rabit.set_error_mode(True)
     try:
         with pytest.raises(TypeError):
-            rabit.allreduce(np.ones(2, dtype=np.float16), rabit.SUM)
+            rabit.allreduce(np.ones(2, dtype=np.int16), rabit.SUM)
         with pytest.raises(TypeError):
             rabit.allreduce(np.ones(2), rabit.BITOR)
     finally:
@@ -104,3 +104,14 @@ def test_fuzz_collectives_with_failures(native_build):
     assert rc == 0, out[-3000:]
     assert out.count("FUZZ OK") == 4, out[-3000:]
     assert sum(a - 1 for a in job.attempts) == 3, job.attempts
+
+
+@pytest.mark.parametrize("extra", [[], ["rabit_reduce_ring_mincount=1"]])
+def test_half_precision_host(native_build, extra):
+    """extended dtypes kHalf / kBFloat16 on the host path (tree and ring)"""
+    job = LocalJob([sys.executable, os.path.join(ROOT, "tests", "scripts", "host_half.py")] +
+                   extra, 3, 1, capture=True, timeout=120, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-3000:]
+    assert out.count("H16 OK") == 3, out[-3000:]

@@ -117,3 +117,15 @@ def test_bench_torchrun_shared_gpu(n):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["transport"]["direct"] == 1, rec
+
+
+@pytest.mark.parametrize("mode", ["pull", "push"])
+def test_direct_half_precision(mode):
+    """bf16 / fp16 allreduce (sum, max, min, fused averaging) on HBM through the direct
+    transport: fp32 accumulation over all ranks, one rounding, bit-exact against torch"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_half.py", 3, ["rabit_device_direct_mode=" + mode])
+    assert rc == 0, out[-5000:]
+    assert out.count("HALF OK") == 3, out[-3000:]
+
