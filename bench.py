@@ -107,6 +107,15 @@ def run_extras(rabit, torch, dev, world):
     out["lazy_sq_64MiB_unfused_us"] = round(_timed(rabit, torch, unfused, 5) * 1e6, 1)
     rabit.checkpoint(None)
     del grad, acc
+    # the headline's 128 MiB as bf16 gradients (extended dtype; fp32 accumulation in the kernels)
+    hb = torch.rand((128 << 20) // 2, device=dev).to(torch.bfloat16)
+    rabit.allreduce(hb, rabit.SUM)
+    t = _timed(rabit, torch, lambda: rabit.allreduce(hb, rabit.SUM), 5)
+    out["allreduce_128MiB_bf16_us"] = round(t * 1e6, 1)
+    out["allreduce_128MiB_bf16_busbw_GBps"] = (round((128 << 20) / t / 1e9 * 2 * (world - 1) / world, 2)
+                                               if world > 1 else None)
+    rabit.checkpoint(None)
+    del hb
     # config 5 (checkpoint part): HBM snapshot of a 256 MiB model every iteration
     model = torch.rand((256 << 20) // 4, dtype=torch.float32, device=dev)
     rabit.checkpoint_tensors({"w": model}, meta={"it": 0})
