@@ -41,12 +41,7 @@ failure case tried is bit-identical to the clean eager run (tools/graph_check.py
 """
 from __future__ import annotations
 
-import os
-
 from typing import Any, Callable, Optional
-
-
-_SYNC_BEFORE_REPLAY = os.environ.get("RABIT_GRAPH_SYNC", "0") == "1"  # diagnostics
 
 
 class GraphedStep:
@@ -75,8 +70,6 @@ class GraphedStep:
         if not self.enabled or not torch.cuda.is_available():
             return self.fn()
         if self.graph is not None:
-            if _SYNC_BEFORE_REPLAY:
-                torch.cuda.synchronize()
             self.graph.replay()
             return self.out
         cur = torch.cuda.current_stream()
