@@ -67,14 +67,24 @@ def main():
         t2 = time.time()
         iter_t.append(t2 - t0)
         ckpt_t.append(t2 - t1)
-    # closed form check: every iteration adds world*(world-1)/2 + 1e-3*world*model
+    # closed form check: the model stays uniform and every iteration maps m to
+    # m * (1 + 1e-3 * world) + world * (world - 1) / 2 (a wrong replay after the failure shows)
+    expect = 0.0
+    for _ in range(iters):
+        expect = expect * (1.0 + 1e-3 * world) + world * (world - 1) / 2.0
+    if gpu:
+        lo, hi = float(model.min().item()), float(model.max().item())
+    else:
+        lo, hi = float(model.min()), float(model.max())
+    model_ok = abs(lo - expect) <= 1e-4 * expect and abs(hi - expect) <= 1e-4 * expect
     st = rabit.stats()
     rec = {"rank": rank, "world": world, "attempt": attempt, "device": gpu,
            "bytes": nbytes, "start_version": version,
            "iter_ms": [round(t * 1e3, 2) for t in iter_t],
            "checkpoint_ms": [round(t * 1e3, 3) for t in ckpt_t],
            "recoveries": st["n_recover_events"], "recovered_ops": st["n_recovered_ops"],
-           "device_replays": st.get("n_device_replays", 0)}
+           "device_replays": st.get("n_device_replays", 0),
+           "model_check": {"ok": model_ok, "expect": expect, "min": lo, "max": hi}}
     if attempt > 0:
         rec["restart_to_loaded_s"] = round(t_loaded - T_START, 3)
     if rank == 0 and iter_t:
@@ -84,6 +94,8 @@ def main():
                           "checkpoint_ms_median": round(float(np.median(ckpt_t)) * 1e3, 3)}
     print("ROBUST " + json.dumps(rec), flush=True)
     rabit.finalize()
+    if not model_ok:
+        sys.exit("rank %d: model %.6g..%.6g, expected %.6g" % (rank, lo, hi, expect))
 
 
 if __name__ == "__main__":
