@@ -111,3 +111,15 @@ def test_mock_hang_detected_by_hang_timeout(native_build):
     assert out.count("PASSED") == 6, out[-4000:]
     assert "Hit Mock Hang" in out and "exiting for a restart" in out, out[-3000:]
     assert job.attempts[3] == 2, job.attempts
+
+
+def test_config5_robust_bench_model_check(native_build):
+    """BASELINE config 5 on the host path (tools/robust_bench.py): allreduce + CheckPoint every
+    iteration, rank 3 killed after checkpoint 2 and restarted; every rank, the restarted one
+    included, must end with the closed-form model."""
+    script = os.path.join(ROOT, "tools", "robust_bench.py")
+    env = {"XR_ITERS": "5", "PYTHONPATH": ROOT}
+    rc, job, out = _run([sys.executable, script, "mock=3,2,0,0"], n=4, attempts=3, env=env)
+    assert rc == 0, out[-4000:]
+    assert out.count('"model_check": {"ok": true') == 4, out[-4000:]
+    assert job.attempts[3] == 2, job.attempts
