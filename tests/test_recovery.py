@@ -123,3 +123,17 @@ def test_config5_robust_bench_model_check(native_build):
     assert rc == 0, out[-4000:]
     assert out.count('"model_check": {"ok": true') == 4, out[-4000:]
     assert job.attempts[3] == 2, job.attempts
+
+
+@pytest.mark.gpu
+def test_config5_robust_bench_model_check_hbm(native_build):
+    """Config 5 on HBM: 4 ranks on GPU 0 (direct transport), 256 MiB device allreduce + HBM
+    checkpoint every iteration, rank 3 killed and reloaded from a survivor's snapshot."""
+    script = os.path.join(ROOT, "tools", "robust_bench.py")
+    env = {"XR_ITERS": "6", "PYTHONPATH": ROOT}
+    rc, job, out = _run([sys.executable, script, "mock=3,3,0,0"], n=4, attempts=3, env=env,
+                        timeout=110)
+    assert rc == 0, out[-4000:]
+    assert out.count('"device": true') == 4, out[-4000:]
+    assert out.count('"model_check": {"ok": true') == 4, out[-4000:]
+    assert job.attempts[3] == 2, job.attempts
