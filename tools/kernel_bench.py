@@ -53,6 +53,11 @@ def main():
     out_small = torch.empty(n // 4, device=dev)
     ai = torch.randint(0, 1 << 30, (n,), generator=g, device=dev, dtype=torch.int32)
     bi = torch.randint(0, 1 << 30, (n,), generator=g, device=dev, dtype=torch.int32)
+    # bf16 operands of the same byte size (fp32 accumulation inside the kernels)
+    ah = torch.rand(2 * n, generator=g, device=dev).to(torch.bfloat16)
+    bh = torch.rand(2 * n, generator=g, device=dev).to(torch.bfloat16)
+    srcs_h = [torch.rand(n // 2, generator=g, device=dev).to(torch.bfloat16) for _ in range(8)]
+    out_small_h = torch.empty(n // 2, device=dev, dtype=torch.bfloat16)
     cases = {
         "rabit_reduce_sum_f32": (lambda: ops.reduce_(a, b, ops.SUM), 3 * S),
         "torch_add_f32": (lambda: a.add_(b), 3 * S),
@@ -68,6 +73,11 @@ def main():
         "torch_stack_sum8_f32": (lambda: torch.sum(torch.stack(srcs), dim=0, out=out_small),
                                  9 * S // 4),
         "rabit_checksum": (lambda: ops.checksum(a), S),
+        "rabit_reduce_sum_bf16": (lambda: ops.reduce_(ah, bh, ops.SUM), 3 * S),
+        "torch_add_bf16": (lambda: ah.add_(bh), 3 * S),
+        "rabit_multi8_sum_bf16": (lambda: ops.reduce_multi(out_small_h, srcs_h, ops.SUM), 9 * S // 4),
+        "torch_stack_sum8_bf16": (lambda: torch.sum(torch.stack(srcs_h), dim=0, out=out_small_h),
+                                  9 * S // 4),
     }
     results = {k: [] for k in cases}
     for _ in range(args.rounds):
