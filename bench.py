@@ -1,11 +1,17 @@
 #!/usr/bin/env python3
 """Headline benchmark of xrabit on MI355X (BASELINE.json): 128 MB float32 Allreduce<Sum>.
 
-Each timed step is one `rabit.allreduce(x, SUM)` of a 128 MB float32 HBM tensor through the
-fault-tolerant (robust) engine: consensus bookkeeping, RCCL/xGMI allreduce written straight
-into the HBM result log, and the copy back into the user tensor (the full per-op work a
-rabit user pays; nothing is skipped).  At N=1 the engine's world-size-1 short-circuit is
-disabled (rabit_world1_fastpath=0) so the step still runs the robust path on the device.
+Each timed step is one `rabit.allreduce(x, SUM)` of a 128 MB float32 HBM tensor (a plain torch
+allocation, as a training job's gradient) through the fault-tolerant (robust) engine: the
+collective over xGMI (RCCL or the direct IPC transport, whichever the start-up calibration
+measured faster) written straight into the HBM result log and the user tensor.  Nothing is
+skipped.
+
+At N > 1 the run also times every transport the job has up, side by side, on torch-allocated
+and on symmetric-heap inputs (RCCL, direct pull, direct push), each first checked bit for bit
+against a host fp64 reference.  At N = 1 no byte moves between ranks: the step is the robust
+engine's bookkeeping plus its HBM result-log copy (rabit_world1_fastpath=0), reported as such
+(`collective: false`); busbw is 0 by definition.
 
     python bench.py                       # N=1
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -13,18 +19,67 @@ disabled (rabit_world1_fastpath=0) so the step still runs the robust path on the
 
 Rank 0 prints one JSON line.  `value` is the whole-job aggregate throughput N * S / t
 (GB/s, S = 128 MiB per rank, weak scaling); nccl-tests style `busbw_GBps` / `algbw_GBps` and
-the per-step wall clock are reported alongside.
+the per-step wall clock are reported alongside.  The whole run is under a wall-clock deadline
+(--deadline): a rank that exceeds it names the phase it was in and exits non-zero.
 """
 import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+PHASE = {"name": "start", "t0": time.time()}
+
+
+def phase(name):
+    PHASE["name"] = name
+
+
+def start_deadline(seconds, rank):
+    """exit non-zero, naming the phase, if the run is not done within `seconds`"""
+    def expire():
+        sys.stderr.write("bench.py: rank %d exceeded its %d s deadline in phase '%s' "
+                         "(%.0f s into the run)\n" % (rank, seconds, PHASE["name"],
+                                                       time.time() - PHASE["t0"]))
+        sys.stderr.flush()
+        os._exit(3)
+    t = threading.Timer(seconds, expire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def pattern_fill(x, rank):
+    """exactly representable float32 data: x[i] = (7 i + 13 rank) mod 1024, so every order of
+    summation over <= 8 ranks gives the same bits"""
+    import torch
+    i = torch.arange(x.numel(), device=x.device, dtype=torch.int64)
+    x.copy_(((i * 7 + 13 * rank) % 1024).to(x.dtype))
+
+
+def host_reference(n, world):
+    """fp64 sum over ranks of pattern_fill, on the host"""
+    i = np.arange(n, dtype=np.int64)
+    acc = np.zeros(n, dtype=np.float64)
+    for r in range(world):
+        acc += ((i * 7 + 13 * r) % 1024).astype(np.float64)
+    return acc
+
+
+def check_allreduce(rabit, x, rank, ref):
+    """one allreduce of the pattern, compared element by element with the host reference;
+    the verdict is agreed over all ranks (max of the failure flags)"""
+    pattern_fill(x, rank)
+    rabit.allreduce(x, rabit.SUM)
+    ok = bool(np.array_equal(x.cpu().numpy().astype(np.float64), ref))
+    bad = rabit.allreduce(np.array([0 if ok else 1], dtype=np.int32), rabit.MAX)[0]
+    return not bad
 
 
 def _timed(rabit, torch, fn, reps, settle=0.0, device_wide=True):
@@ -127,6 +182,58 @@ def run_extras(rabit, torch, dev, world):
     return out
 
 
+def time_steps(rabit, torch, x, steps):
+    """wall time of `steps` back-to-back allreduces, ranks in lock step, max over ranks"""
+    torch.cuda.synchronize()
+    rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rabit.allreduce(x, rabit.SUM)
+    torch.cuda.synchronize()
+    rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    return float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
+
+
+def run_variants(rabit, torch, dev, n, world, rank, ref, steps):
+    """every transport this job has up, on torch-allocated and symmetric-heap inputs: time
+    and busbw of the 128 MiB float32 sum, each checked against the host fp64 reference"""
+    out = []
+    bufs = [("torch", torch.empty(n, dtype=torch.float32, device=dev))]
+    try:
+        bufs.append(("symmetric", rabit.symmetric_empty(n, torch.float32)))
+    except MemoryError:
+        pass
+    variants = [("rccl", rabit.TRANSPORT_RCCL, None), ("direct-pull", rabit.TRANSPORT_DIRECT, "pull"),
+                ("direct-push", rabit.TRANSPORT_DIRECT, "push")]
+    for input_name, x in bufs:
+        for name, which, mode in variants:
+            phase("variant %s/%s" % (name, input_name))
+            up = rabit.set_device_transport(which, mode)
+            # the same choice on every rank, or none
+            up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
+            rec = {"transport": name, "input": input_name, "available": bool(up)}
+            if up:
+                rec["check"] = check_allreduce(rabit, x, rank, ref)
+                x.copy_(torch.rand(n, device=dev).mul_(1e-3))
+                for _ in range(2):
+                    rabit.allreduce(x, rabit.SUM)
+                t = time_steps(rabit, torch, x, steps) / steps
+                rec["t_us"] = round(t * 1e6, 1)
+                rec["algbw_GBps"] = round(n * 4 / t / 1e9, 2)
+                rec["busbw_GBps"] = round(n * 4 / t / 1e9 * 2 * (world - 1) / world, 2)
+                rabit.checkpoint(None)  # bounded result log
+            out.append(rec)
+    rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
+    st = rabit.stats()
+    if st.get("device_direct"):
+        # back to the calibrated pull/push choice
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st.get("direct_push") else "pull")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,15 +242,18 @@ def main():
     ap.add_argument("--size-mb", type=int, default=128)
     ap.add_argument("--engine", default="robust", choices=["robust", "base"])
     ap.add_argument("--check", type=int, default=1, help="verify one reduction first")
-    ap.add_argument("--symmetric", type=int, default=-1,
-                    help="allocate the buffer in rabit's symmetric heap (IPC-registered HBM that "
-                         "the direct transport reads in place, like registered buffers in "
-                         "nccl-tests); 0: a plain torch allocation (staged through a copy); "
-                         "-1 (default): symmetric when N > 1 (at N=1 nothing is exchanged)")
+    ap.add_argument("--symmetric", type=int, default=0,
+                    help="1: the headline buffer lives in rabit's symmetric heap (IPC-registered "
+                         "HBM the direct transport reads in place, like registered buffers in "
+                         "nccl-tests); 0 (default): a plain torch allocation")
+    ap.add_argument("--variants", type=int, default=1,
+                    help="N > 1: also time every transport on torch and symmetric-heap inputs")
     ap.add_argument("--extras", type=int, default=1,
                     help="after the timed loop, also time the other BASELINE configs: 1 GiB "
                          "broadcast, 64 MiB lazy (squared-gradient) allreduce fused vs unfused, "
                          "256 MiB HBM checkpoint")
+    ap.add_argument("--deadline", type=int, default=900,
+                    help="wall-clock limit of the whole run in seconds")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -152,6 +262,8 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: launch N>1 with "
                          "torch.distributed.run" % (args.gpus, world))
+    timer = start_deadline(args.deadline, rank)
+    phase("import")
     import torch
     import rabit_amd as rabit
     from rabit_amd.torchrun import init_from_env
@@ -163,51 +275,46 @@ def main():
     gpu = local_rank % ngpu
     shared_gpu = ngpu < int(os.environ.get("LOCAL_WORLD_SIZE", world))
     torch.cuda.set_device(gpu)
-    # the rabit tracker lives in rank 0 next to the torchrun master port (rabit_amd.torchrun)
     n = args.size_mb * (1 << 20) // 4
-    if args.symmetric < 0:
-        args.symmetric = 1 if world > 1 else 0
-    # + 48 MiB: the calibration's 32 MiB inputs come from the heap's free tail, so it times the
-    # paths heap buffers take
-    heap = {"rabit_device_symmetric_heap": str(n * 4 + (48 << 20))} if args.symmetric else {}
+    # the symmetric heap holds the variant matrix's second buffer (+ 48 MiB: the calibration's
+    # 32 MiB inputs come from the heap's free tail when it has one)
+    heap_bytes = n * 4 + (48 << 20) if (world > 1 and args.variants) or args.symmetric else 0
+    heap = {"rabit_device_symmetric_heap": str(heap_bytes)} if heap_bytes else {}
+    phase("init")
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
                         rabit_world1_fastpath=0, rabit_device=gpu, **heap)
     dev = torch.device("cuda", gpu)
 
-    def barrier():
-        rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
-
+    phase("reference")
+    ref = host_reference(n, world) if args.check or args.variants else None
     if args.symmetric:
         x = rabit.symmetric_empty(n, torch.float32)
     else:
         x = torch.empty(n, dtype=torch.float32, device=dev)
+    checked = None
     if args.check:
-        x.fill_(float(rabit.get_rank() + 1))
-        rabit.allreduce(x, rabit.SUM)
-        expect = world * (world + 1) / 2.0
-        ok = bool(torch.all(x == expect).item())
-        bad = rabit.allreduce(np.array([0 if ok else 1], dtype=np.int32), rabit.SUM)[0]
-        if bad:
-            raise SystemExit("allreduce result check failed on %d rank(s)" % bad)
+        phase("check")
+        checked = check_allreduce(rabit, x, rank, ref)
+        if not checked:
+            raise SystemExit("allreduce result check against the host fp64 reference failed")
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     # |x| ~ 1e-3 keeps repeated in-place sums finite for hundreds of 8-rank steps
     x.copy_(torch.rand((n,), generator=g, dtype=torch.float32, device=dev).mul_(1e-3))
 
+    phase("warmup")
     for _ in range(args.warmup):
         rabit.allreduce(x, rabit.SUM)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rabit.allreduce(x, rabit.SUM)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
+    phase("timed")
+    elapsed = time_steps(rabit, torch, x, args.steps)
+    st_head = rabit.stats()
 
+    variants = None
+    if world > 1 and args.variants:
+        phase("variants")
+        rabit.checkpoint(None)
+        variants = run_variants(rabit, torch, dev, n, world, rank, ref, max(5, args.steps // 2))
+    phase("extras")
     extras = run_extras(rabit, torch, dev, world) if args.extras else {}
 
     t_step = elapsed / args.steps
@@ -215,7 +322,7 @@ def main():
     algbw = size_bytes / t_step / 1e9
     busbw = algbw * (2.0 * (world - 1) / world) if world > 1 else 0.0
     aggregate = world * size_bytes / t_step / 1e9
-    st = rabit.stats()
+    st = st_head
     rec = {
         "metric": "allreduce_128MB_fp32_sum_throughput",
         "value": round(aggregate, 2),
@@ -236,9 +343,11 @@ def main():
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "t_us": round(t_step * 1e6, 1),
+        "collective": world > 1,
         "value_definition": "N * bytes_per_rank / t_step (whole-job reduced bytes per second); "
                             "busbw = algbw * 2(N-1)/N as nccl-tests",
         "baseline_note": "reference publishes no numbers (BASELINE.md)",
+        "result_check": "bit-exact vs host fp64 reference" if checked else None,
         "consensus_elided": st.get("n_consensus_elided", 0),
         "device_epoch": st.get("device_epoch", 0),
         "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),
@@ -247,16 +356,24 @@ def main():
                       "calibration_us": st.get("calib_us"),
                       "direct_variant": "push" if st.get("direct_push") else "pull",
                       "calibration_push_us": st.get("calib_push_us"),
-                      "calibration_heap_inputs": bool(st.get("calib_heap_src", 0))},
+                      "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),
+                      "peer_links": st.get("peer_links")},
+        "variants": variants,
         "extras": extras,
         "reference_measured": reference_measured(world, aggregate),
     }
+    if world == 1:
+        rec["n1_note"] = ("N=1: no data moves between ranks; the step is the robust engine's "
+                          "per-op bookkeeping plus its HBM result-log copy (robust-path overhead, "
+                          "not a collective)")
     if shared_gpu:
         rec["shared_gpu_rehearsal"] = "%d ranks on %d GPU(s): not an xGMI measurement" % (world, ngpu)
     if rank == 0:
         print(json.dumps(rec), flush=True)
+    phase("finalize")
     del x
     ctx.finalize()
+    timer.cancel()
 
 
 if __name__ == "__main__":

@@ -82,12 +82,31 @@ RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes
 RABIT_DLL int RabitDevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                      char **out_meta, rbt_ulong *out_meta_len);
 /*!
+ * \brief RabitDevCheckPoint plus this rank's local model as nl HBM buffers: kept (with the
+ *        replicas of the rabit_local_replica ring predecessors) in HBM and replicated over
+ *        xGMI by the robust engine
+ */
+RABIT_DLL void RabitDevCheckPointEx(int n, void *const *ptrs, const size_t *nbytes,
+                                    const char *meta, rbt_ulong meta_len, int nl,
+                                    void *const *lptrs, const size_t *lnbytes);
+/*! \brief RabitDevLoadCheckPoint that also fills the nl local-model buffers */
+RABIT_DLL int RabitDevLoadCheckPointEx(int n, void *const *ptrs, const size_t *nbytes,
+                                       char **out_meta, rbt_ulong *out_meta_len, int nl,
+                                       void *const *lptrs, const size_t *lnbytes);
+/*!
  * \brief allocate nbytes from the engine's symmetric heap (rabit_device_symmetric_heap=<size>):
  *        HBM that the peers map through IPC, so an allreduce input placed there is read in
  *        place by the direct transport (no stage copy).  NULL when unavailable or full; the
  *        memory lives until RabitFinalize.
  */
 RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes);
+/*!
+ * \brief benchmarking / diagnosis: route device collectives of this rank over one transport
+ *        (which: -1 calibrated choice, 0 RCCL, 1 direct) and pick the direct reduce-scatter
+ *        variant (direct_mode: 0 unchanged, 1 pull, 2 push).  Every rank must make the same
+ *        call between the same collectives.  -1 when the transport is not up.
+ */
+RABIT_DLL int RabitDevSetTransport(int which, int direct_mode);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

@@ -238,20 +238,49 @@ RABIT_DLL void RabitDevCheckPoint(int n, void *const *ptrs, const size_t *nbytes
   });
 }
 
+RABIT_DLL void RabitDevCheckPointEx(int n, void *const *ptrs, const size_t *nbytes,
+                                    const char *meta, rbt_ulong meta_len, int nl,
+                                    void *const *lptrs, const size_t *lnbytes) {
+  GuardVoid([&]() {
+    rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+    rabit::utils::Check(e != nullptr, "device checkpoint needs a tracker-backed engine");
+    e->DevCheckPoint(n, ptrs, nbytes, std::string(meta == nullptr ? "" : meta, meta_len), nl,
+                     lptrs, lnbytes);
+  });
+}
+
 RABIT_DLL int RabitDevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                      char **out_meta, rbt_ulong *out_meta_len) {
+  return RabitDevLoadCheckPointEx(n, ptrs, nbytes, out_meta, out_meta_len, 0, nullptr, nullptr);
+}
+
+RABIT_DLL int RabitDevLoadCheckPointEx(int n, void *const *ptrs, const size_t *nbytes,
+                                       char **out_meta, rbt_ulong *out_meta_len, int nl,
+                                       void *const *lptrs, const size_t *lnbytes) {
   static thread_local std::string meta;
   return Guard(
       [&]() {
         rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
         rabit::utils::Check(e != nullptr, "device checkpoint needs a tracker-backed engine");
         meta.clear();
-        const int v = e->DevLoadCheckPoint(n, ptrs, nbytes, &meta);
+        const int v = e->DevLoadCheckPoint(n, ptrs, nbytes, &meta, nl, lptrs, lnbytes);
         *out_meta = rabit::BeginPtr(meta);
         *out_meta_len = static_cast<rbt_ulong>(meta.size());
         return v;
       },
       -1);
+}
+
+RABIT_DLL int RabitDevSetTransport(int which, int direct_mode) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) return -1;
+  rabit::device::DevicePlane *d = e->device_plane();
+  if (which == 0 && !d->has_comm()) return -1;
+  if (which == 1 && !d->has_peers()) return -1;
+  if (direct_mode != 0 && !d->has_peers()) return -1;
+  d->ForceTransport(which);
+  if (direct_mode != 0) d->SetDirectPush(direct_mode == 2);
+  return 0;
 }
 
 RABIT_DLL const char *RabitGetLastError() { return g_last_error.c_str(); }

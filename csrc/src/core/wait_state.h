@@ -28,6 +28,7 @@ struct WaitState {
   std::atomic<int> op_depth{0};        // > 0: inside a public collective / checkpoint
   std::atomic<int> wait_depth{0};      // > 0: blocked on peers, the device or the tracker
   std::atomic<double> working_since{0};  // start of the current working stretch (0: none)
+  std::atomic<double> device_wait_since{0};  // start of the current wait on the GPU (0: none)
 };
 
 inline WaitState &GlobalWaitState() {
@@ -69,6 +70,33 @@ class WaitScope {
   WaitScope(const WaitScope &) = delete;
   WaitScope &operator=(const WaitScope &) = delete;
 };
+
+/*!
+ * \brief marks a host wait on this rank's GPU work (stream drain, blocking copies, collective
+ *        completion); the watchdog terminates a rank whose wait exceeds the device wait limit,
+ *        which covers HIP calls that block without any deadline of their own
+ */
+class DeviceWaitScope {
+ public:
+  DeviceWaitScope() {
+    double zero = 0.0;
+    outer_ = GlobalWaitState().device_wait_since.compare_exchange_strong(zero, MonotonicSec());
+  }
+  ~DeviceWaitScope() {
+    if (outer_) GlobalWaitState().device_wait_since.store(0.0);
+  }
+  DeviceWaitScope(const DeviceWaitScope &) = delete;
+  DeviceWaitScope &operator=(const DeviceWaitScope &) = delete;
+
+ private:
+  bool outer_{false};
+};
+
+/*! \brief seconds this rank has been waiting on its GPU (0: not waiting) */
+inline double DeviceWaitingFor() {
+  const double since = GlobalWaitState().device_wait_since.load();
+  return since > 0 ? MonotonicSec() - since : 0.0;
+}
 
 /*! \brief seconds this rank has been working inside an op without waiting (0: not) */
 inline double WorkingFor() {

@@ -7,13 +7,16 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
 
 #include "core/wait_state.h"
 #include "device/kernels.h"
+#include "rabit/internal/half.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -68,6 +71,10 @@ size_t TypeBytes(int dtype) {
   }
 }
 }  // namespace
+
+// pinned word that ends an injected hang; process-wide so that the watchdog thread and the
+// exit path can release it without touching the plane
+std::atomic<int *> g_hang_release{nullptr};
 
 // ------------------------------------------------------------------ arena
 DeviceArena::~DeviceArena() {
@@ -243,10 +250,118 @@ void DevicePlane::AbortComm() {
     ncclCommAbort(comm_);
     comm_ = nullptr;
   }
-  if (peers_ != nullptr) {
-    (void)hipStreamSynchronize(stream_);
-    peers_.reset();
+  // whatever was in flight must now end: aborted RCCL kernels and barriers return promptly;
+  // a stream that does not drain holds work of this rank that will never finish
+  if (!DrainStream(cfg_.drain_timeout_sec)) {
+    WedgedExit("the device stream did not drain after the communicators were aborted");
   }
+  peers_.reset();
+}
+
+void DevicePlane::InjectHang(double max_sec) {
+  int *w = g_hang_release.load();
+  if (w == nullptr) {
+    void *p = nullptr;
+    CheckHip(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped),
+             "hipHostMalloc(hang word)");
+    w = static_cast<int *>(p);
+    g_hang_release.store(w);
+  }
+  __atomic_store_n(w, 0, __ATOMIC_SEQ_CST);
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_);
+  const long long ticks = static_cast<long long>(max_sec * khz * 1000.0);
+  CheckHip(LaunchHang(w, ticks, stream_), "LaunchHang");
+}
+
+void DevicePlane::ReleaseHang() {
+  int *w = g_hang_release.load();
+  if (w != nullptr) __atomic_store_n(w, 1, __ATOMIC_SEQ_CST);
+}
+
+bool DevicePlane::DrainStream(double sec) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(stream_);
+    if (e == hipSuccess) return true;
+    if (e != hipErrorNotReady) {
+      (void)hipGetLastError();
+      return true;  // a failed stream is not a hung one: the error surfaces on its next use
+    }
+    if (std::chrono::duration<double>(clock::now() - t0).count() > sec) return false;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+}
+
+void DevicePlane::WedgedExit(const char *why) {
+  fprintf(stderr, "xrabit: %s: device stream wedged, exiting for a restart\n", why);
+  fflush(stderr);
+  ReleaseHang();
+  // a released injected hang and the guarded kernels behind it retire within microseconds;
+  // give them that time before the process and its queues go away (no blocking HIP call here:
+  // a really wedged stream would never return from it)
+  std::this_thread::sleep_for(std::chrono::milliseconds(200));
+  std::_Exit(kDeviceHangExitCode);
+}
+
+bool DevicePlane::Preflight(const std::vector<PeerRecord> &all, int rank, std::string *why) {
+  links_.clear();
+  char mine[32] = {0};
+  (void)hipDeviceGetPCIBusId(mine, sizeof(mine), device_);
+  bool ok = true;
+  for (int r = 0; r < static_cast<int>(all.size()); ++r) {
+    if (r == rank) continue;
+    PeerLinkInfo li;
+    li.rank = r;
+    char pci[sizeof(all[r].pci) + 1] = {0};
+    std::memcpy(pci, all[r].pci, sizeof(all[r].pci));
+    li.same_gpu = std::strncmp(pci, mine, sizeof(mine)) == 0;
+    int ord = -1;
+    if (pci[0] != '\0' && hipDeviceGetByPCIBusId(&ord, pci) == hipSuccess) {
+      li.ordinal = ord;
+    } else {
+      (void)hipGetLastError();
+    }
+    if (li.ordinal >= 0 && !li.same_gpu) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, device_, li.ordinal) == hipSuccess) {
+        li.can_access = can;
+      } else {
+        (void)hipGetLastError();
+      }
+      uint32_t type = 0, hops = 0;
+      if (hipExtGetLinkTypeAndHopCount(device_, li.ordinal, &type, &hops) == hipSuccess) {
+        li.link_type = static_cast<int>(type);
+        li.hops = static_cast<int>(hops);
+      } else {
+        (void)hipGetLastError();
+      }
+      if (li.can_access == 0 && ok) {
+        ok = false;
+        *why = "GPU " + std::to_string(device_) + " cannot access the GPU of rank " +
+               std::to_string(r) + " (" + pci + ")";
+      }
+    }
+    links_.push_back(li);
+  }
+  return ok;
+}
+
+std::string DevicePlane::PeerLinksJson() const {
+  std::string out = "[";
+  for (size_t i = 0; i < links_.size(); ++i) {
+    const PeerLinkInfo &l = links_[i];
+    const char *type = l.same_gpu ? "same_gpu"
+                                  : (l.link_type == 4 ? "xgmi"
+                                                      : (l.link_type == 2 ? "pcie" : "unknown"));
+    char buf[192];
+    snprintf(buf, sizeof(buf),
+             "%s{\"rank\":%d,\"ordinal\":%d,\"can_access\":%d,\"link\":\"%s\",\"hops\":%d}",
+             i ? "," : "", l.rank, l.ordinal, l.can_access, type, l.hops);
+    out += buf;
+  }
+  return out + "]";
 }
 
 void DevicePlane::DescribeDevice(PeerRecord *rec) const {
@@ -294,7 +409,10 @@ bool DevicePlane::DirectPhaseUs(double out[PeerGroup::kPhases], uint64_t *nops) 
 
 void DevicePlane::DropPeers() {
   if (peers_ != nullptr) {
-    (void)hipStreamSynchronize(stream_);
+    if (!DrainStream(cfg_.drain_timeout_sec)) {
+      peers_->SignalAbort();
+      if (!DrainStream(cfg_.drain_timeout_sec)) WedgedExit("dropping the direct transport");
+    }
     peers_.reset();
   }
 }
@@ -317,8 +435,10 @@ void DevicePlane::EnterFromUser() {
 
 Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
   core::WaitScope waiting;  // peers' barriers and RCCL: waiting on other ranks
+  core::DeviceWaitScope on_gpu;
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
+  const double limit = cfg_.op_timeout_sec < 0 ? AutoOpDeadline(op_bytes_) : cfg_.op_timeout_sec;
   for (uint64_t iter = 0;; ++iter) {
     hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) {
@@ -346,15 +466,13 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
     }
     const double waited = std::chrono::duration<double>(clock::now() - t0).count();
     if (probe && (iter & 63) == 0 && waited > 1e-3 && probe()) {
-      AbortComm();
-      (void)hipStreamSynchronize(stream_);
+      AbortComm();  // drains the stream, or ends the process if this rank's work is wedged
       return Status::kAborted;
     }
-    if (cfg_.op_timeout_sec > 0 && waited > cfg_.op_timeout_sec) {
-      utils::HandleLogInfo("[xrabit] device op exceeded %.1f s, aborting communicator\n",
-                           cfg_.op_timeout_sec);
+    if (limit > 0 && waited > limit) {
+      utils::HandleLogInfo("[xrabit] device op (%zu B) exceeded its %.1f s deadline, aborting "
+                           "the communicators\n", op_bytes_, limit);
       AbortComm();
-      (void)hipStreamSynchronize(stream_);
       return Status::kTimeout;
     }
     // spin first: the wake-up latency after completion sits on the critical path of every op
@@ -366,6 +484,7 @@ Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
   CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
   Status s = Status::kSuccess;
   if (cfg_.sync && host_wait) s = WaitEvent(ev_done_, probe);
+  op_bytes_ = 0;
   if (pending_dst_ != nullptr) {
     if (s == Status::kSuccess) {
       CopyDeviceAsync(pending_dst_, pending_src_, pending_bytes_);
@@ -381,6 +500,7 @@ Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
 
 void DevicePlane::Synchronize() {
   core::WaitScope waiting;
+  core::DeviceWaitScope on_gpu;
   CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
@@ -407,11 +527,13 @@ void *DevicePlane::Scratch(size_t bytes, int slot) {
 }
 
 void DevicePlane::StageToHost(void *host, const void *dev, size_t bytes) {
+  core::DeviceWaitScope on_gpu;
   CheckHip(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
   CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 void DevicePlane::StageToDevice(void *dev, const void *host, size_t bytes) {
+  core::DeviceWaitScope on_gpu;
   CheckHip(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream_), "H2D");
   CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
@@ -419,6 +541,7 @@ void DevicePlane::StageToDevice(void *dev, const void *host, size_t bytes) {
 Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype,
                               int op, int prep, double alpha, const FailureProbe &probe) {
   const size_t bytes = count * TypeBytes(dtype);
+  op_bytes_ = bytes;
   if (UseDirect(bytes)) {
     CheckHip(peers_->Allreduce(send, recv, recv2, count, dtype, op, prep, alpha),
              "direct allreduce");
@@ -428,12 +551,35 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   ncclDataType_t t;
   ncclRedOp_t o;
   if (!RcclType(dtype, &t)) utils::Error("unsupported dtype %d on device", dtype);
-  if (prep != kPrepCopy) {
+  // a scaling prepare of a floating sum rides on RCCL's pre-multiplied sum (no extra pass)
+  const bool premul = prep == kPrepScale && op == 2 &&
+                      (dtype == 6 || dtype == 7 || dtype == 10 || dtype == 11);
+  if (prep != kPrepCopy && !premul) {
     CheckHip(LaunchPrepare(recv, nullptr, send, count, dtype, prep, alpha, stream_),
              "LaunchPrepare");
     send = recv;
   }
-  if (!RcclOp(op, &o)) {
+  if (premul) {
+    ncclRedOp_t pm;
+    double a64 = alpha;
+    float a32 = static_cast<float>(alpha);
+    // fp16/bf16 scalars are passed as the element type by RCCL: convert on the host
+    uint16_t a16 = 0;
+    void *scalar = &a32;
+    if (dtype == 7) {
+      scalar = &a64;
+    } else if (dtype == 10) {
+      a16 = half_t::FromFloat(a32);
+      scalar = &a16;
+    } else if (dtype == 11) {
+      a16 = bf16_t::FromFloat(a32);
+      scalar = &a16;
+    }
+    CheckNccl(ncclRedOpCreatePreMulSum(&pm, scalar, t, ncclScalarHostImmediate, comm_),
+              "ncclRedOpCreatePreMulSum");
+    CheckNccl(ncclAllReduce(send, recv, count, t, pm, comm_, stream_), "ncclAllReduce");
+    CheckNccl(ncclRedOpDestroy(pm, comm_), "ncclRedOpDestroy");
+  } else if (!RcclOp(op, &o)) {
     PeerGroup::ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
                                              const int *guard, const void *const *table,
                                              double post, hipStream_t st) {
@@ -463,6 +609,7 @@ Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, s
     return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
   };
   const size_t bytes = count * type_nbytes;
+  op_bytes_ = bytes;
   if (UseDirect(bytes)) {
     CheckHip(peers_->AllreduceCustom(send, recv, recv2, count, type_nbytes, step),
              "direct allreduce (custom)");
@@ -484,51 +631,70 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
   (void)probe;
   utils::Check(comm_ != nullptr, "device allreduce without communicator");
   const int n = nranks_;
-  // all-to-all: rank k receives everyone's copy of segment k, reduces it with the
-  // multi-source kernel, then an allgather distributes the reduced segments
-  const size_t seg = (count + n - 1) / n;
-  const size_t seg_bytes = ((seg * tn + 255) / 256) * 256;  // keep segments 256-B aligned
-  char *a = static_cast<char *>(Scratch(seg_bytes * n, 0));
-  char *b = static_cast<char *>(Scratch(seg_bytes * n, 1));
-  // pack the input as n segments of seg_bytes
+  // reduce-scatter + allgather as two rounds of grouped point-to-point copies that read and
+  // write the buffers in place (segments are whole 256-element blocks, so every segment start
+  // is as aligned as the buffer): no packing into scratch, no unpacking afterwards
+  const size_t seg = ((count + n - 1) / n + 255) / 256 * 256;
+  auto lo = [&](int k) { return std::min(count, seg * static_cast<size_t>(k)); };
+  auto hi = [&](int k) { return std::min(count, seg * static_cast<size_t>(k + 1)); };
+  const char *in = static_cast<const char *>(send);
+  char *out = static_cast<char *>(recv);
+  const size_t mine = hi(rank_) - lo(rank_);
+  const size_t slot = (mine * tn + 255) / 256 * 256;
+  char *inbox = static_cast<char *>(Scratch(std::max<size_t>(slot * n, 256), 1));
+  // 1. segment k of every rank's input goes to rank k
+  CheckNccl(ncclGroupStart(), "ncclGroupStart");
   for (int k = 0; k < n; ++k) {
-    const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
-    if (hi > lo) {
-      CheckHip(LaunchCopy(a + k * seg_bytes, static_cast<const char *>(send) + lo * tn,
-                          (hi - lo) * tn, stream_),
-               "pack");
+    if (k == rank_) continue;
+    if (hi(k) > lo(k)) {
+      CheckNccl(ncclSend(in + lo(k) * tn, (hi(k) - lo(k)) * tn, ncclUint8, k, comm_, stream_),
+                "ncclSend");
+    }
+    if (mine != 0) {
+      CheckNccl(ncclRecv(inbox + static_cast<size_t>(k) * slot, mine * tn, ncclUint8, k, comm_,
+                         stream_),
+                "ncclRecv");
     }
   }
-  CheckNccl(ncclAllToAll(a, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllToAll");
-  // reduce the n copies of my segment, up to 8 sources per kernel pass
-  char *mine = a + static_cast<size_t>(rank_) * seg_bytes;
-  std::vector<const void *> srcs;
-  int done = 0;
-  while (done < n) {
-    srcs.clear();
-    if (done > 0) srcs.push_back(mine);
-    while (done < n && static_cast<int>(srcs.size()) < kMaxReduceSources) {
-      srcs.push_back(b + static_cast<size_t>(done) * seg_bytes);
-      ++done;
+  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+  // 2. reduce the n copies of my segment (rank order, up to 8 sources per pass) into place
+  if (mine != 0) {
+    std::vector<const void *> srcs;
+    int done = 0;
+    char *dst = out + lo(rank_) * tn;
+    while (done < n) {
+      srcs.clear();
+      if (done > 0) srcs.push_back(dst);
+      while (done < n && static_cast<int>(srcs.size()) < kMaxReduceSources) {
+        srcs.push_back(done == rank_ ? static_cast<const void *>(in + lo(rank_) * tn)
+                                     : inbox + static_cast<size_t>(done) * slot);
+        ++done;
+      }
+      CheckHip(step(dst, srcs.data(), static_cast<int>(srcs.size()), mine, nullptr, nullptr, 0.0,
+                    stream_),
+               "allreduce reduce step");
     }
-    CheckHip(step(mine, srcs.data(), static_cast<int>(srcs.size()), seg, nullptr, nullptr, 0.0,
-                  stream_),
-             "allreduce reduce step");
   }
-  CheckNccl(ncclAllGather(mine, b, seg_bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+  // 3. every reduced segment to every rank, straight into its place in recv
+  CheckNccl(ncclGroupStart(), "ncclGroupStart");
   for (int k = 0; k < n; ++k) {
-    const size_t lo = std::min(count, k * seg), hi = std::min(count, (k + 1) * seg);
-    if (hi > lo) {
-      CheckHip(LaunchCopy(static_cast<char *>(recv) + lo * tn, b + k * seg_bytes,
-                          (hi - lo) * tn, stream_),
-               "unpack");
+    if (k == rank_) continue;
+    if (mine != 0) {
+      CheckNccl(ncclSend(out + lo(rank_) * tn, mine * tn, ncclUint8, k, comm_, stream_),
+                "ncclSend");
+    }
+    if (hi(k) > lo(k)) {
+      CheckNccl(ncclRecv(out + lo(k) * tn, (hi(k) - lo(k)) * tn, ncclUint8, k, comm_, stream_),
+                "ncclRecv");
     }
   }
+  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
   return Status::kSuccess;
 }
 
 Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe) {
   (void)probe;
+  op_bytes_ = bytes;
   if (UseDirect(bytes)) {
     CheckHip(peers_->Broadcast(buf, bytes, root), "direct broadcast");
     return Status::kSuccess;
@@ -538,9 +704,45 @@ Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailurePr
   return Status::kSuccess;
 }
 
+Status DevicePlane::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in) {
+  *bytes_in = 0;
+  op_bytes_ = 0;
+  for (const ExchangeItem &x : plan) op_bytes_ += x.bytes;
+  const bool direct = peers_ != nullptr && (comm_ == nullptr || force_ == 1);
+  if (direct) {
+    CheckHip(peers_->Exchange(plan, bytes_in), "direct exchange");
+    return Status::kSuccess;
+  }
+  // a copy to itself is a local kernel; the rest pairs up as ncclSend / ncclRecv
+  bool any = false;
+  for (const ExchangeItem &x : plan) {
+    if (x.bytes == 0) continue;
+    if (x.src == rank_ && x.dst == rank_) {
+      CopyDeviceAsync(x.dst_ptr, x.src_ptr, x.bytes);
+    } else if (x.src == rank_ || x.dst == rank_) {
+      any = true;
+    }
+  }
+  if (!any) return Status::kSuccess;
+  utils::Check(comm_ != nullptr, "device exchange without a transport");
+  CheckNccl(ncclGroupStart(), "ncclGroupStart");
+  for (const ExchangeItem &x : plan) {
+    if (x.bytes == 0 || x.src == x.dst) continue;
+    if (x.src == rank_) {
+      CheckNccl(ncclSend(x.src_ptr, x.bytes, ncclUint8, x.dst, comm_, stream_), "ncclSend");
+    } else if (x.dst == rank_) {
+      CheckNccl(ncclRecv(x.dst_ptr, x.bytes, ncclUint8, x.src, comm_, stream_), "ncclRecv");
+      *bytes_in += x.bytes;
+    }
+  }
+  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+  return Status::kSuccess;
+}
+
 Status DevicePlane::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
                                const std::vector<size_t> &size, const FailureProbe &probe) {
   (void)probe;
+  op_bytes_ = total;
   if (UseDirect(total)) {
     CheckHip(peers_->AllgatherV(buf_, total, begin, size), "direct allgather");
     return Status::kSuccess;

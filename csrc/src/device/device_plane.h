@@ -39,9 +39,10 @@ typedef std::function<bool()> FailureProbe;
 struct DeviceConfig {
   int device{-1};                      // -1: LOCAL_RANK env, else rank % device count
   bool sync{true};                     // host waits for each collective to complete
-  double op_timeout_sec{0};            // 0: no deadline on a device op
+  double op_timeout_sec{-1};           // deadline of a device op: < 0 auto (size-scaled), 0 none
+  double drain_timeout_sec{30};        // after an abort, the stream must drain within this
   size_t arena_chunk{256u << 20};      // result-log arena growth step
-  size_t arena_cap{size_t(64) << 30};  // beyond this the result log falls back to host memory
+  size_t arena_cap{size_t(64) << 30};  // beyond this the result log spills to pinned host memory
   int spin_us{5000};                   // busy-poll window before sleeping while waiting
   int algo{0};                         // 0 auto, 1 RCCL only, 2 direct (IPC peer memory) only
   size_t peer_stage{256u << 20};       // direct transport: bytes per stage buffer (x2 per rank)
@@ -53,6 +54,12 @@ struct DeviceConfig {
   size_t oneshot_max{256u << 10};      // direct allreduce: one-shot up to this many bytes
   int direct_mode{0};                  // direct reduce-scatter: 0 calibrated, 1 pull, 2 push
 };
+
+/*! \brief exit status of a rank whose own device stream stayed wedged after an abort (the
+ *  launcher restarts it; its peers recover as from a crash) */
+constexpr int kDeviceHangExitCode = 251;
+/*! \brief auto deadline of a device op of this many bytes: 60 s plus 1 s per GB */
+inline double AutoOpDeadline(size_t bytes) { return 60.0 + static_cast<double>(bytes) * 1e-9; }
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
  *  chunks; Reset() keeps the chunks so steady-state iterations never call hipMalloc) */
@@ -142,6 +149,26 @@ class DevicePlane {
     ++epoch_;
   }
 
+  // ---- peer preflight (before the direct transport maps anything)
+  /*! \brief what this rank found out about the link to one peer */
+  struct PeerLinkInfo {
+    int rank{-1};
+    int ordinal{-1};      // the peer's GPU as this process numbers it (-1: not visible)
+    int can_access{-1};   // hipDeviceCanAccessPeer (-1: not checked)
+    int link_type{-1};    // hipExtGetLinkTypeAndHopCount: 4 = xGMI, 2 = PCIe (-1: unknown)
+    int hops{-1};
+    bool same_gpu{false};
+  };
+  /*!
+   * \brief map every peer's GPU (by PCI bus id) to a local ordinal, check peer access and the
+   *        link type; false (with why) if a visible peer GPU cannot be accessed, in which case
+   *        the direct transport must stay off (RCCL only)
+   */
+  bool Preflight(const std::vector<PeerRecord> &all, int rank, std::string *why);
+  const std::vector<PeerLinkInfo> &peer_links() const { return links_; }
+  /*! \brief links_ as a JSON array */
+  std::string PeerLinksJson() const;
+
   // ---- direct transport (IPC peer memory over xGMI)
   /*! \brief allocate and export the local stage buffers; false (with why) if impossible */
   bool PreparePeers(PeerRecord *rec, std::string *why);
@@ -203,9 +230,36 @@ class DevicePlane {
   /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place */
   Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                     const std::vector<size_t> &size, const FailureProbe &probe);
+  /*!
+   * \brief point-to-point copies over xGMI (see ExchangeItem; every rank passes the same plan).
+   *        With RCCL: one grouped ncclSend/ncclRecv call on the ranks that take part (the others
+   *        do nothing); otherwise the direct transport's stage exchange.  Enqueue only: the
+   *        caller waits with Finish().  *bytes_in: payload bytes this rank received from peers.
+   */
+  Status Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in);
   /*! \brief stage a host-reducer allreduce through pinned host memory */
   void StageToHost(void *host, const void *dev, size_t bytes);
   void StageToDevice(void *dev, const void *host, size_t bytes);
+
+  // ---- device failure handling
+  /*!
+   * \brief fault injection (mock_dev_hang): enqueue a kernel that wedges this stream (it ignores
+   *        aborts) for at most max_sec; the collective queued behind it never starts
+   */
+  void InjectHang(double max_sec);
+  /*! \brief end an injected hang (also called from the watchdog thread) */
+  static void ReleaseHang();
+  /*! \brief poll until the plane stream is idle; false after sec seconds */
+  bool DrainStream(double sec);
+  /*!
+   * \brief this rank's own device work does not finish even after the communicators were
+   *        aborted: end the process with kDeviceHangExitCode for a restart (the peers see the
+   *        links drop and recover as from a crash).  Injected hangs are released first so that
+   *        no wave outlives the process.
+   */
+  [[noreturn]] static void WedgedExit(const char *why);
+  /*! \brief bytes of the op being waited for (auto deadline) */
+  void set_op_bytes(size_t b) { op_bytes_ = b; }
 
   // ---- memory / ordering
   /*! \brief async copy on the plane stream (any memory kinds) */
@@ -248,6 +302,8 @@ class DevicePlane {
   size_t scratch_bytes_[kScratchSlots]{0, 0, 0};
   void *pinned_{nullptr};
   size_t pinned_bytes_{0};
+  size_t op_bytes_{0};
+  std::vector<PeerLinkInfo> links_;
 };
 
 /*! \brief throw rabit::Error on a HIP failure */

@@ -54,6 +54,12 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
 /*! \brief device-to-device copy: 16-byte-per-lane kernel for the aligned bulk (the blit
  *  kernel behind hipMemcpyAsync D2D streams slower), hipMemcpyAsync for an unaligned rest */
 hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stream);
+/*!
+ * \brief fault injection (mock_dev_hang): a one-wave kernel that models a wedged kernel on the
+ *        stream.  It ignores the engine's abort word; it ends when the host sets *release or
+ *        after max_ticks of the device wall clock, so no wave outlives the process.
+ */
+hipError_t LaunchHang(const volatile int *release, long long max_ticks, hipStream_t stream);
 /*! \brief fill count elements with value (bit pattern of dtype) */
 hipError_t LaunchFill(void *dst, size_t count, int dtype, double value, hipStream_t stream);
 }  // namespace device

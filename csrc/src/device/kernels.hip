@@ -511,6 +511,13 @@ __global__ __launch_bounds__(kBlock) void FillKernel(T *dst, size_t n, T value) 
   if (i < n) dst[i] = value;
 }
 
+// ---------------------------------------------------------------- fault injection
+__global__ __launch_bounds__(64) void HangKernel(const volatile int *release, long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  while (*release == 0 && wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // dtype code -> C++ type; integer-only ops reject float types
 template <typename Fn>
 hipError_t DispatchType(int dtype, bool int_only, Fn &&fn) {
@@ -642,6 +649,11 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
                      static_cast<const uint4 *>(buf), nvec, partial);
   hipLaunchKernelGGL(ChecksumFinishKernel, dim3(1), dim3(kBlock), 0, stream,
                      static_cast<const unsigned long long *>(partial), static_cast<int>(grid), out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchHang(const volatile int *release, long long max_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(HangKernel, dim3(1), dim3(64), 0, stream, release, max_ticks);
   return hipGetLastError();
 }
 

@@ -483,6 +483,89 @@ hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size
   }
   return hipSuccess;
 }
+hipError_t PeerGroup::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in) {
+  utils::Assert(opened_, "peer group not opened");
+  *bytes_in = 0;
+  // every sender's distinct payloads, back to back (256-B aligned) in plan order: the byte
+  // stream it pushes through its stage buffer.  All ranks derive the same layout.
+  std::vector<size_t> stream_len(n_, 0), at(plan.size(), 0);
+  std::vector<std::vector<std::pair<int, size_t>>> first(n_);  // (key, offset) per sender
+  for (size_t i = 0; i < plan.size(); ++i) {
+    const ExchangeItem &x = plan[i];
+    utils::Check(x.src >= 0 && x.src < n_ && x.dst >= 0 && x.dst < n_,
+                 "device exchange: rank out of range");
+    if (x.src == x.dst || x.bytes == 0) continue;
+    auto &seen = first[x.src];
+    auto it = std::find_if(seen.begin(), seen.end(),
+                           [&](const std::pair<int, size_t> &p) { return p.first == x.key; });
+    if (it != seen.end()) {
+      at[i] = it->second;
+      continue;
+    }
+    at[i] = stream_len[x.src];
+    seen.emplace_back(x.key, at[i]);
+    stream_len[x.src] += RoundUp(x.bytes, 256);
+  }
+  CopyBatch b;
+  NewBatch(&b);
+  auto add = [&](char *dst, const char *src, size_t bytes) -> hipError_t {
+    if (bytes == 0) return hipSuccess;
+    if (b.n == kMaxCopySegs) {
+      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+      NewBatch(&b);
+    }
+    AddSeg(&b, dst, src, nullptr, bytes);
+    return hipSuccess;
+  };
+  auto flush = [&]() -> hipError_t {
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    NewBatch(&b);
+    return hipSuccess;
+  };
+  // copies a rank makes to itself never touch the stage
+  for (const ExchangeItem &x : plan) {
+    if (x.src == rank_ && x.dst == rank_) {
+      XRABIT_TRY_HIP(add(static_cast<char *>(x.dst_ptr), static_cast<const char *>(x.src_ptr),
+                         x.bytes));
+    }
+  }
+  XRABIT_TRY_HIP(flush());
+  size_t rounds = 0;
+  for (int s = 0; s < n_; ++s) rounds = std::max(rounds, (stream_len[s] + stage_bytes_ - 1) / stage_bytes_);
+  for (size_t r = 0; r < rounds; ++r) {
+    const size_t lo = r * stage_bytes_, hi = lo + stage_bytes_;
+    const int which = parity_;
+    parity_ ^= 1;
+    // 1. my window of my stream into my stage (each distinct payload once)
+    std::vector<int> staged;
+    for (size_t i = 0; i < plan.size(); ++i) {
+      const ExchangeItem &x = plan[i];
+      if (x.src != rank_ || x.dst == rank_ || x.bytes == 0) continue;
+      if (std::find(staged.begin(), staged.end(), x.key) != staged.end()) continue;
+      staged.push_back(x.key);
+      const size_t a = std::max(lo, at[i]), z = std::min(hi, at[i] + x.bytes);
+      if (z > a) {
+        XRABIT_TRY_HIP(add(stage(rank_, which) + (a - lo),
+                           static_cast<const char *>(x.src_ptr) + (a - at[i]), z - a));
+      }
+    }
+    XRABIT_TRY_HIP(flush());
+    XRABIT_TRY_HIP(Barrier());
+    // 2. pull the parts of this window addressed to me
+    for (size_t i = 0; i < plan.size(); ++i) {
+      const ExchangeItem &x = plan[i];
+      if (x.dst != rank_ || x.src == rank_ || x.bytes == 0) continue;
+      const size_t a = std::max(lo, at[i]), z = std::min(hi, at[i] + x.bytes);
+      if (z > a) {
+        XRABIT_TRY_HIP(add(static_cast<char *>(x.dst_ptr) + (a - at[i]),
+                           stage(x.src, which) + (a - lo), z - a));
+        *bytes_in += z - a;
+      }
+    }
+    XRABIT_TRY_HIP(flush());
+  }
+  return hipSuccess;
+}
 #undef XRABIT_TRY_HIP
 }  // namespace device
 }  // namespace rabit

@@ -105,6 +105,19 @@ struct PeerRecord {
   uint64_t heap_bytes;
 };
 
+/*!
+ * \brief one point-to-point copy of a device exchange (every rank passes the same global plan;
+ *        src_ptr is only meaningful on rank src, dst_ptr only on rank dst).  Items of one
+ *        sender with the same key carry the same bytes (sent once, read by several receivers).
+ */
+struct ExchangeItem {
+  int src, dst;
+  int key;
+  size_t bytes;
+  const void *src_ptr;
+  void *dst_ptr;
+};
+
 /*! \brief this rank's symmetric heap (owned by the DevicePlane, outlives peer groups) */
 struct SymHeapInfo {
   char *base{nullptr};
@@ -146,6 +159,15 @@ class PeerGroup {
   hipError_t Broadcast(void *buf, size_t bytes, int root);
   hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                         const std::vector<size_t> &size);
+  /*!
+   * \brief point-to-point copies between ranks (a collective: every rank passes the same plan).
+   *        Each sender streams the distinct payloads it owns through its stage buffer, one
+   *        stage-sized window per round; after the round's barrier every receiver pulls the
+   *        parts addressed to it from the senders' stages.  Ranks that neither send nor receive
+   *        only join the barriers (no payload bytes move through them).
+   *        *bytes_in receives the payload bytes this rank pulled from peers.
+   */
+  hipError_t Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in);
 
   /*! \brief make spinning barriers give up (host side; safe at any time) */
   void SignalAbort();

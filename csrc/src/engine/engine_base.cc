@@ -63,7 +63,13 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device")) dcfg_.device = atoi(val);
   if (is("rabit_device_plane")) device_plane_mode_ = utils::StringToBool(val) ? 1 : 0;
   if (is("rabit_device_sync")) dcfg_.sync = utils::StringToBool(val);
-  if (is("rabit_device_timeout_sec")) dcfg_.op_timeout_sec = atof(val);
+  if (is("rabit_device_timeout_sec")) {
+    // "auto" (default): 60 s + 1 s per GB of the op; 0: no deadline
+    dcfg_.op_timeout_sec = strcmp(val, "auto") == 0 ? -1.0 : atof(val);
+  }
+  if (is("rabit_device_drain_timeout_sec")) dcfg_.drain_timeout_sec = atof(val);
+  if (is("rabit_device_wait_limit_sec")) dev_wait_limit_sec_ = atof(val);
+  if (is("rabit_mock_dev_hang_sec")) dev_hang_max_sec_ = atof(val);
   if (is("rabit_device_spin_us")) dcfg_.spin_us = atoi(val);
   if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
@@ -347,9 +353,13 @@ Status EngineBase::EnsureDeviceComm() {
                             std::strncmp(all[r].pci, all[q].pci, sizeof(rec.pci)) == 0);
     }
   }
-  // 2. direct transport: map the peers' buffers; every rank must succeed (min-allreduce)
+  // 2. direct transport: check that every visible peer GPU is reachable (peer access, link
+  //    type), then map the peers' buffers; every rank must succeed (min-allreduce), otherwise
+  //    the job runs on RCCL alone
   int ok = 0;
-  if (have_peers && all_peers && same_host) {
+  const bool reachable = dev_->Preflight(all, rank_, &why);
+  if (!reachable) utils::HandleLogInfo("[%d] direct transport off: %s\n", rank_, why.c_str());
+  if (have_peers && all_peers && same_host && reachable) {
     ok = dev_->OpenPeers(all, rank_, &why) ? 1 : 0;
     if (!ok) utils::HandleLogInfo("[%d] direct transport: %s\n", rank_, why.c_str());
   }
@@ -547,6 +557,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     }
     Status s = EnsureDeviceComm();
     if (s != Status::kSuccess) return s;
+    MaybeInjectDeviceHang();
     s = dev_->AllreduceCustom(src, dst, dst2, spec.count, spec.type_nbytes, spec.dev_red,
                               MakeProbe());
     if (s != Status::kSuccess) return s;
@@ -581,6 +592,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   }
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
+  MaybeInjectDeviceHang();
   s = dev_->Allreduce(src, dst, dst2, spec.count, spec.dtype, spec.op, prep, alpha, MakeProbe());
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
@@ -606,6 +618,7 @@ Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
   if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
   dev_->EnterFromUser();
+  MaybeInjectDeviceHang();
   s = dev_->Broadcast(buf, size, root, MakeProbe());
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
@@ -656,6 +669,7 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
   if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
   dev_->EnterFromUser();
+  MaybeInjectDeviceHang();
   s = dev_->AllgatherV(buf, total, b, z, MakeProbe());
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
@@ -763,11 +777,36 @@ void EngineBase::Allgather(void *buf, size_t total, size_t begin, size_t end, si
 
 int EngineBase::LoadCheckPoint(Serializable *, Serializable *) { return 0; }
 
+namespace {
+/*! \brief force_local: the global tensors join the local model, the global checkpoint keeps
+ *  only the metadata (the mock engine's stress test of local replication) */
+void FoldIntoLocal(int *n, void *const **ptrs, const size_t **nbytes, int *nl,
+                   void *const **lptrs, const size_t **lnbytes, std::vector<void *> *pbuf,
+                   std::vector<size_t> *sbuf) {
+  pbuf->assign(*ptrs, *ptrs + *n);
+  sbuf->assign(*nbytes, *nbytes + *n);
+  pbuf->insert(pbuf->end(), *lptrs, *lptrs + *nl);
+  sbuf->insert(sbuf->end(), *lnbytes, *lnbytes + *nl);
+  *nl = static_cast<int>(pbuf->size());
+  *lptrs = pbuf->data();
+  *lnbytes = sbuf->data();
+  *n = 0;
+}
+}  // namespace
+
 void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
-                               const std::string &meta) {
+                               const std::string &meta, int nl, void *const *lptrs,
+                               const size_t *lnbytes) {
   utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
+  std::vector<void *> pbuf;
+  std::vector<size_t> sbuf;
+  if (ForceLocal()) FoldIntoLocal(&n, &ptrs, &nbytes, &nl, &lptrs, &lnbytes, &pbuf, &sbuf);
   for (int i = 0; i < n; ++i) {
     utils::Check(nbytes[i] == 0 || OnDevice(ptrs[i]), "device checkpoint: buffer %d not in HBM", i);
+  }
+  for (int i = 0; i < nl; ++i) {
+    utils::Check(lnbytes[i] == 0 || OnDevice(lptrs[i]),
+                 "device checkpoint: local buffer %d not in HBM", i);
   }
   device::DeviceGuard dg(dev_->device());
   if (!dev_ckpt_) {
@@ -776,20 +815,48 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
   }
   trace::Scope ts("device_snapshot", rank_, version_number_, seq_counter_, 0, 1);
   const Serializable *snap = dev_ckpt_->Snapshot(n, ptrs, nbytes, meta);
-  this->LazyCheckPoint(snap);
+  dev_local_.owner = this;
+  dev_local_.Set(nl, lptrs, lnbytes);
+  this->CheckPointDevice(snap, nl > 0 ? &dev_local_ : nullptr);
 }
 
 int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
-                                  std::string *meta) {
+                                  std::string *meta, int nl, void *const *lptrs,
+                                  const size_t *lnbytes) {
   utils::Check(dev_ != nullptr, "device checkpoint needs the device plane");
+  std::vector<void *> pbuf;
+  std::vector<size_t> sbuf;
+  if (ForceLocal()) FoldIntoLocal(&n, &ptrs, &nbytes, &nl, &lptrs, &lnbytes, &pbuf, &sbuf);
   device::DeviceGuard dg(dev_->device());
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_always(ckpt_mirror_always_);
   }
-  const int version = this->LoadCheckPoint(dev_ckpt_->Loader(n, ptrs, nbytes), nullptr);
+  dev_local_.owner = this;
+  dev_local_.Set(nl, lptrs, lnbytes);
+  const int version =
+      this->LoadCheckPoint(dev_ckpt_->Loader(n, ptrs, nbytes), nl > 0 ? &dev_local_ : nullptr);
   if (version > 0 && meta != nullptr) *meta = dev_ckpt_->loaded_meta();
   return version;
+}
+
+void EngineBase::DeviceLocalModel::Save(Stream *fo) const {
+  // host staging (engines without an HBM replica store)
+  std::vector<char> tmp;
+  for (size_t i = 0; i < ptrs.size(); ++i) {
+    tmp.resize(nbytes[i]);
+    if (nbytes[i] != 0) owner->dev_->StageToHost(tmp.data(), ptrs[i], nbytes[i]);
+    fo->Write(tmp.data(), nbytes[i]);
+  }
+}
+
+void EngineBase::DeviceLocalModel::Load(Stream *fi) {
+  std::vector<char> tmp;
+  for (size_t i = 0; i < ptrs.size(); ++i) {
+    tmp.resize(nbytes[i]);
+    utils::Check(fi->Read(tmp.data(), nbytes[i]) == nbytes[i], "device local model: short read");
+    if (nbytes[i] != 0) owner->dev_->StageToDevice(ptrs[i], tmp.data(), nbytes[i]);
+  }
 }
 
 void EngineBase::CheckPoint(const Serializable *, const Serializable *) {
@@ -820,7 +887,8 @@ std::string EngineBase::StatsJson() const {
      << ",\"calib_push_us\":" << calib_.push_big * 1e6
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
-     << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0);
+     << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)
+     << ",\"peer_links\":" << (dev_ ? dev_->PeerLinksJson() : std::string("[]"));
   double phase[device::PeerGroup::kPhases];
   uint64_t nphase = 0;
   if (dev_ && dev_->DirectPhaseUs(phase, &nphase)) {
@@ -837,6 +905,8 @@ std::string EngineBase::StatsJson() const {
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
      << ",\"n_device_replays\":" << s.n_device_replays
      << ",\"n_device_ckpt_loads\":" << s.n_device_ckpt_loads
+     << ",\"bytes_local_in\":" << s.bytes_local_in << ",\"bytes_replay_in\":" << s.bytes_replay_in
+     << ",\"bytes_ckpt_in\":" << s.bytes_ckpt_in
      << ",\"bytes_allreduce\":" << s.bytes_allreduce
      << ",\"bytes_broadcast\":" << s.bytes_broadcast
      << ",\"bytes_allgather\":" << s.bytes_allgather << ",\"t_allreduce\":" << s.t_allreduce

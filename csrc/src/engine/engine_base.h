@@ -36,7 +36,10 @@ struct EngineStats {
   uint64_t n_shm_ops{0};
   uint64_t n_consensus_elided{0};
   uint64_t n_device_replays{0};
-  uint64_t n_device_ckpt_loads{0};  // checkpoint loads served by device broadcasts  // results recovered by a device broadcast (one xGMI hop)
+  uint64_t n_device_ckpt_loads{0};  // checkpoint loads served over the device plane
+  double bytes_local_in{0};   // local-checkpoint replica bytes received over the device plane
+  double bytes_replay_in{0};  // recovered result bytes received over the device plane
+  double bytes_ckpt_in{0};    // global-checkpoint bytes received over the device plane
   double bytes_allreduce{0}, bytes_broadcast{0}, bytes_allgather{0};
   double t_allreduce{0}, t_broadcast{0}, t_allgather{0}, t_checkpoint{0}, t_consensus{0};
   double t_recover{0};
@@ -93,11 +96,23 @@ class EngineBase : public IEngine {
                                     const char *_caller);
   /*!
    * \brief checkpoint HBM buffers: HBM snapshot + async pinned mirror, registered as a lazy
-   *        global checkpoint (see device/device_checkpoint.h)
+   *        global checkpoint (see device/device_checkpoint.h).  nl > 0: lptrs are this rank's
+   *        local model (per-rank state): the robust engine keeps it, and the replicas of its
+   *        ring predecessors, in HBM and replicates it over xGMI.
    */
-  void DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes, const std::string &meta);
-  /*! \brief load the latest device checkpoint into HBM buffers; returns the version */
-  int DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes, std::string *meta);
+  void DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes, const std::string &meta,
+                     int nl = 0, void *const *lptrs = nullptr, const size_t *lnbytes = nullptr);
+  /*! \brief load the latest device checkpoint into HBM buffers (and the local model into
+   *         lptrs when nl > 0); returns the version */
+  int DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes, std::string *meta,
+                        int nl = 0, void *const *lptrs = nullptr, const size_t *lnbytes = nullptr);
+  /*! \brief register a device checkpoint (global snapshot, optional device local model) */
+  virtual void CheckPointDevice(const Serializable *global_model, const Serializable *local_model) {
+    (void)local_model;
+    this->LazyCheckPoint(global_model);
+  }
+  /*! \brief mock engine's force_local: global tensors are checkpointed as local state too */
+  virtual bool ForceLocal() const { return false; }
   /*! \brief engine statistics as JSON */
   virtual std::string StatsJson() const;
   device::DevicePlane *device_plane() { return dev_.get(); }
@@ -154,9 +169,38 @@ class EngineBase : public IEngine {
   bool PeerFailureProbe() const;
   /*! \brief Hadoop status line */
   void ReportStatus() const;
+  /*! \brief mock_dev_hang: wedge this rank's stream before the next device collective */
+  void MaybeInjectDeviceHang() {
+    if (!dev_hang_armed_) return;
+    dev_hang_armed_ = false;
+    dev_->InjectHang(dev_hang_max_sec_);
+  }
   device::FailureProbe MakeProbe() const {
     return [this]() { return this->PeerFailureProbe(); };
   }
+
+  /*!
+   * \brief HBM tensors that form this rank's local model in a device checkpoint.  The robust
+   *        engine recognises this object and moves its bytes HBM to HBM; Save/Load (host
+   *        staging) serve engines that keep local state in host memory.
+   */
+  struct DeviceLocalModel : public Serializable {
+    EngineBase *owner{nullptr};
+    std::vector<void *> ptrs;
+    std::vector<size_t> nbytes;
+    size_t total() const {
+      size_t t = 0;
+      for (size_t b : nbytes) t += b;
+      return t;
+    }
+    void Set(int n, void *const *p, const size_t *b) {
+      ptrs.assign(p, p + n);
+      nbytes.assign(b, b + n);
+    }
+    void Load(Stream *fi) override;
+    void Save(Stream *fo) const override;
+  };
+  DeviceLocalModel dev_local_;
 
   // parameters / configuration
   std::vector<std::string> env_vars_;
@@ -193,6 +237,9 @@ class EngineBase : public IEngine {
     double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes, push_big;
   } calib_{0, 0, 0, 0, 0, 0, 0};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
+  bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
+  double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long
+  double dev_wait_limit_sec_{600};  // watchdog: a wait on this rank's GPU may last this long
   bool trace_spans_{false};
   bool trace_roctx_{false};
   size_t trace_capacity_{1 << 16};

@@ -8,8 +8,10 @@
  * rabit::Error (as the reference); the C API turns an uncaught error into process exit,
  * which is what the launcher's restart logic observes.
  * Extensions: `mock_hang=rank,version,seqno,ntrial` makes the rank stop responding (sleeps
- * forever) instead of dying, to exercise the timeout watchdog; `force_local` and
- * `report_stats` behave as in the reference.
+ * forever) instead of dying, to exercise the timeout watchdog; `mock_dev_hang=...` keeps the
+ * process alive but wedges its GPU stream right before the device collective (a hung kernel:
+ * the peers' barriers / RCCL time out, the rank finds its own stream stuck after the abort and
+ * exits for a restart); `force_local` and `report_stats` behave as in the reference.
  */
 #ifndef XRABIT_ENGINE_ENGINE_MOCK_H_
 #define XRABIT_ENGINE_ENGINE_MOCK_H_
@@ -37,12 +39,12 @@ class EngineMock : public EngineRobust {
     }
     if (!strcmp(name, "report_stats")) report_stats_ = atoi(val);
     if (!strcmp(name, "force_local")) force_local_ = atoi(val);
-    if (!strcmp(name, "mock") || !strcmp(name, "mock_hang")) {
+    if (!strcmp(name, "mock") || !strcmp(name, "mock_hang") || !strcmp(name, "mock_dev_hang")) {
       Key k;
       utils::Check(sscanf(val, "%d,%d,%d,%d", &std::get<0>(k), &std::get<1>(k), &std::get<2>(k),
                           &std::get<3>(k)) == 4,
                    "invalid mock parameter \"%s\" (expected rank,version,seqno,ntrial)", val);
-      mock_map_[k] = !strcmp(name, "mock_hang") ? 2 : 1;
+      mock_map_[k] = !strcmp(name, "mock_hang") ? 2 : (!strcmp(name, "mock_dev_hang") ? 3 : 1);
     }
   }
   const char *EngineName() const override { return "mock"; }
@@ -97,7 +99,10 @@ class EngineMock : public EngineRobust {
   int LoadCheckPoint(Serializable *global_model, Serializable *local_model) override {
     tsum_allreduce_ = tsum_allgather_ = 0.0;
     time_checkpoint_ = utils::GetTime();
-    if (force_local_ == 0) return EngineRobust::LoadCheckPoint(global_model, local_model);
+    // device checkpoints fold force_local in DevLoadCheckPoint (the local tensors stay in HBM)
+    if (force_local_ == 0 || local_model == &dev_local_) {
+      return EngineRobust::LoadCheckPoint(global_model, local_model);
+    }
     Dummy dum;
     Combo com(global_model, local_model);
     return EngineRobust::LoadCheckPoint(&dum, &com);
@@ -118,7 +123,7 @@ class EngineMock : public EngineRobust {
     if (report_stats_ != 0 && rank_ == 0) {
       std::ostringstream ss;
       ss << "[v" << version_number_ << "] global_size=" << global_checkpoint_.length()
-         << ",local_size=" << (local_chkpt_[0].length() + local_chkpt_[1].length())
+         << ",local_size=" << (local_.configured() ? local_.Bytes(0) + local_.Bytes(1) : 0)
          << ",check_tcost=" << cost << " sec,allreduce_tcost=" << tsum_allreduce_
          << " sec,allgather_tcost=" << tsum_allgather_ << " sec,between_chpt=" << between
          << "sec\n";
@@ -126,6 +131,11 @@ class EngineMock : public EngineRobust {
     }
     tsum_allreduce_ = tsum_allgather_ = 0.0;
   }
+  void CheckPointDevice(const Serializable *global_model, const Serializable *local_model) override {
+    Verify("CheckPoint");
+    EngineRobust::CheckPointDevice(global_model, local_model);
+  }
+  bool ForceLocal() const override { return force_local_ != 0; }
   void LazyCheckPoint(const Serializable *global_model) override {
     Verify("LazyCheckPoint");
     EngineRobust::LazyCheckPoint(global_model);
@@ -163,6 +173,14 @@ class EngineMock : public EngineRobust {
     auto it = mock_map_.find(Key(rank_, version_number_, seq_counter_, num_trial_));
     if (it == mock_map_.end()) return;
     num_trial_ += 1;
+    if (it->second == 3) {
+      // the process stays alive and responsive on the host; its GPU stream wedges right before
+      // this collective, so its peers wait at the device barrier / in RCCL for it
+      fprintf(stderr, "[%d]@@@Hit Mock Device Hang:%s\n", rank_, what);
+      fflush(stderr);
+      dev_hang_armed_ = true;
+      return;
+    }
     if (it->second == 2) {
       core::OpScope in_op;  // the hang is inside the collective (rabit_hang_timeout_sec)
       fprintf(stderr, "[%d]@@@Hit Mock Hang:%s\n", rank_, what);

@@ -165,7 +165,9 @@ bool EngineRobust::Init(int argc, char *argv[]) {
   result_buffer_round_ =
       num_global_replica_ == 0 ? -1 : std::max(GetWorldSize() / num_global_replica_, 1);
   if (dev_) resbuf_.SetArena(dev_->arena());
-  if (timeout_enabled_ || hang_timeout_sec_ > 0) StartWatchdog();
+  if (timeout_enabled_ || hang_timeout_sec_ > 0 || (dev_ && dev_wait_limit_sec_ > 0)) {
+    StartWatchdog();
+  }
   return true;
 }
 
@@ -465,11 +467,15 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
 }
 
 // ------------------------------------------------------------------ checkpoints
-void EngineRobust::LocalModelCheck(bool with_local) {
+void EngineRobust::LocalModelCheck(const Serializable *local_model) {
+  const bool with_local = local_model != nullptr;
   if (use_local_model_ == -1) {
     if (with_local) {
       use_local_model_ = 1;
       if (num_local_replica_ == 0) num_local_replica_ = default_local_replica_;
+      // local tensors stay in HBM (replicated over xGMI); Serializable models in host memory
+      const bool on_device = local_model == &dev_local_ && dev_ != nullptr;
+      local_.Configure(num_local_replica_ + 1, on_device, on_device ? dev_->device() : -1);
     } else {
       use_local_model_ = 0;
       num_local_replica_ = 0;
@@ -478,14 +484,59 @@ void EngineRobust::LocalModelCheck(bool with_local) {
     utils::Check(use_local_model_ == static_cast<int>(with_local),
                  "CheckPoint/LoadCheckPoint must always be called either with or without "
                  "local_model, not both");
+    if (with_local) {
+      utils::Check(local_.on_device() == (local_model == &dev_local_),
+                   "the local model must always be HBM tensors or always a host model");
+    }
   }
+}
+
+void EngineRobust::SaveLocalState(int v, const Serializable *local_model) {
+  local_.Clear(v);
+  if (local_.on_device()) {
+    // the tensors, back to back, into slot 0 (HBM to HBM on the plane stream)
+    device::DeviceGuard dg(dev_->device());
+    dev_->EnterFromUser();
+    local_.BeforeWrite(v, dev_->stream());
+    char *dst = static_cast<char *>(local_.Alloc(v, 0, dev_local_.total()));
+    for (size_t i = 0; i < dev_local_.ptrs.size(); ++i) {
+      if (dev_local_.nbytes[i] == 0) continue;
+      dev_->CopyDeviceAsync(dst, dev_local_.ptrs[i], dev_local_.nbytes[i]);
+      dst += dev_local_.nbytes[i];
+    }
+    return;
+  }
+  std::string *host = local_.HostSlot(v, 0);
+  utils::MemoryBufferStream fs(host);
+  if (local_model != nullptr) local_model->Save(&fs);
+  local_.Alloc(v, 0, host->size());
+}
+
+void EngineRobust::LoadLocalState(int v, Serializable *local_model) {
+  if (local_.on_device()) {
+    utils::Check(static_cast<size_t>(local_.size(v, 0)) == dev_local_.total(),
+                 "[%d] local checkpoint holds %lld bytes, the local tensors %zu", rank_,
+                 static_cast<long long>(local_.size(v, 0)), dev_local_.total());
+    device::DeviceGuard dg(dev_->device());
+    dev_->EnterFromUser();
+    const char *src = static_cast<const char *>(local_.Data(v, 0));
+    for (size_t i = 0; i < dev_local_.ptrs.size(); ++i) {
+      if (dev_local_.nbytes[i] == 0) continue;
+      dev_->CopyDeviceAsync(dev_local_.ptrs[i], src, dev_local_.nbytes[i]);
+      src += dev_local_.nbytes[i];
+    }
+    utils::Check(dev_->Finish(MakeProbe(), false) == Status::kSuccess, "local state load");
+    return;
+  }
+  utils::MemoryFixSizeBuffer fs(local_.Data(v, 0), static_cast<size_t>(local_.size(v, 0)));
+  local_model->Load(&fs);
 }
 
 int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local_model) {
   core::OpScope op_scope;
   checkpoint_loaded_ = true;
   if (GetWorldSize() == 1 && world1_fastpath_) return 0;
-  LocalModelCheck(local_model != nullptr);
+  LocalModelCheck(local_model);
   if (num_local_replica_ == 0) {
     utils::Check(local_model == nullptr,
                  "need to set rabit_local_replica larger than 1 to checkpoint local_model");
@@ -494,13 +545,10 @@ int EngineRobust::LoadCheckPoint(Serializable *global_model, Serializable *local
   trace::Scope ts("load_checkpoint", rank_, version_number_, seq_counter_, 0, 0);
   if (RecoverExec(nullptr, 0, ActionSummary::kLoadCheck, ActionSummary::kSpecialOp,
                   cur_cache_seq_, "LoadCheckPoint")) {
-    const int nlocal =
-        std::max(static_cast<int>(local_rptr_[local_chkpt_version_].size()) - 1, 0);
+    const int nlocal = local_.configured() ? local_.Count(local_chkpt_version_) : 0;
     if (local_model != nullptr) {
       if (nlocal == num_local_replica_ + 1) {
-        utils::MemoryFixSizeBuffer fs(BeginPtr(local_chkpt_[local_chkpt_version_]),
-                                      local_rptr_[local_chkpt_version_][1]);
-        local_model->Load(&fs);
+        LoadLocalState(local_chkpt_version_, local_model);
       } else {
         utils::Assert(nlocal == 0, "[%d] local model inconsistent, nlocal=%d", rank_, nlocal);
       }
@@ -549,28 +597,26 @@ void EngineRobust::CheckPointImpl(const Serializable *global_model,
   }
   const double t0 = utils::GetTime();
   trace::Scope ts("checkpoint", rank_, version_number_, seq_counter_, 0, 0);
-  LocalModelCheck(local_model != nullptr);
+  LocalModelCheck(local_model);
   if (num_local_replica_ == 0) {
     utils::Check(local_model == nullptr,
                  "need to set rabit_local_replica larger than 1 to checkpoint local_model");
   }
   if (num_local_replica_ != 0) {
+    // the new version is written next to the acknowledged one, which stays loadable until
+    // every rank has passed kLocalCheckAck
+    const int nv = !local_chkpt_version_;
     for (;;) {
       if (RecoverExec(nullptr, 0, 0, ActionSummary::kLocalCheckPoint, cur_cache_seq_,
                       "CheckPoint")) {
         break;
       }
-      const int nv = !local_chkpt_version_;
-      local_chkpt_[nv].clear();
-      utils::MemoryBufferStream fs(&local_chkpt_[nv]);
-      if (local_model != nullptr) local_model->Save(&fs);
-      local_rptr_[nv].clear();
-      local_rptr_[nv].push_back(0);
-      local_rptr_[nv].push_back(local_chkpt_[nv].length());
-      if (CheckAndRecover(TryCheckinLocalState(&local_rptr_[nv], &local_chkpt_[nv]))) break;
+      SaveLocalState(nv, local_model);
+      if (CheckAndRecover(TryCheckinLocalState(nv))) break;
     }
     RecoverExec(nullptr, 0, 0, ActionSummary::kLocalCheckAck, cur_cache_seq_, "CheckPoint");
-    local_chkpt_version_ = !local_chkpt_version_;
+    local_chkpt_version_ = nv;
+    if (local_.on_device()) local_.Mirror(nv, dev_->stream());
   }
   utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckPoint, ActionSummary::kSpecialOp,
                            cur_cache_seq_, "CheckPoint"),
@@ -683,6 +729,14 @@ void EngineRobust::WatchdogLoop() {
               wd_rank_.load(), working, hang_timeout_sec_);
       fflush(stderr);
       std::_Exit(kHangExitCode);
+    }
+    // a wait on this rank's own GPU that outlasts every deadline (a HIP call that blocks on a
+    // wedged stream): nothing in this process can unblock it, so leave for a restart
+    const double on_gpu = core::DeviceWaitingFor();
+    if (dev_wait_limit_sec_ > 0 && on_gpu > dev_wait_limit_sec_) {
+      fprintf(stderr, "[%d] xrabit: waiting on the GPU for %.1f s (rabit_device_wait_limit_sec=%g)\n",
+              wd_rank_.load(), on_gpu, dev_wait_limit_sec_);
+      device::DevicePlane::WedgedExit("watchdog");
     }
     const double since = recovering_since_.load();
     if (timeout_enabled_ && since > 0 && utils::GetTime() - since > timeout_sec_ &&

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "engine/engine_base.h"
+#include "engine/local_replicas.h"
 
 namespace rabit {
 namespace engine {
@@ -56,6 +57,9 @@ class EngineRobust : public EngineBase {
                  const int _line, const char *_caller) override;
   void InitAfterException() override;
   int LoadCheckPoint(Serializable *global_model, Serializable *local_model) override;
+  void CheckPointDevice(const Serializable *global_model, const Serializable *local_model) override {
+    CheckPointImpl(global_model, local_model, true);
+  }
   void CheckPoint(const Serializable *global_model, const Serializable *local_model) override {
     CheckPointImpl(global_model, local_model, false);
   }
@@ -188,13 +192,28 @@ class EngineRobust : public EngineBase {
   /*! \brief checkpoint load over the device plane (see recovery.cc); kAborted: not applicable */
   Status TryLoadDeviceCheckPoint(RecoverType role);
   Status TryGetResult(void *buf, size_t size, int seqno, bool requester);
+  /*! \brief per-rank role bits of a device recovery transfer, gathered on every rank */
+  static constexpr int kReplayCapable = 1, kReplayHolder = 2, kReplayRequester = 4;
+  Status GatherCodes(int mine, std::vector<int> *all);
   Status TryDecideRouting(RecoverType role, size_t *p_size, int *p_recvlink,
                           std::vector<bool> *p_req_in);
   Status TryRecoverData(RecoverType role, void *buf, size_t size, int recv_link,
                         const std::vector<bool> &req_in);
   Status TryRestoreCache(bool requester, int min_seq, int max_seq);
-  Status TryRecoverLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt);
-  Status TryCheckinLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt);
+  /*!
+   * \brief local state of version v (engine/local_recovery.cc): every rank learns every rank's
+   *        slot sizes over TCP, then each missing slot is copied in one hop from a rank that
+   *        holds that state (device store: one xGMI exchange; host store: routed over the tree)
+   */
+  Status TryRecoverLocalState(int v);
+  /*! \brief replicate this rank's slot 0 of version v to its num_local_replica successors */
+  Status TryCheckinLocalState(int v);
+  /*! \brief n x (nslot + 1) table: slot sizes of version v per rank, then the store kind */
+  Status GatherLocalSizes(int v, std::vector<int64_t> *table);
+  /*! \brief write the local model into slot 0 of version v (the other slots are dropped) */
+  void SaveLocalState(int v, const Serializable *local_model);
+  /*! \brief load slot 0 of version v into the local model */
+  void LoadLocalState(int v, Serializable *local_model);
   /*!
    * \brief two-pass message passing over the tree: out[i] = func(node, in[others], i) is sent
    *        on link i, in[i] is what link i sent (reference allreduce_robust-inl.h:33-166)
@@ -202,7 +221,9 @@ class EngineRobust : public EngineBase {
   template <typename NodeT, typename EdgeT>
   Status MsgPassing(const NodeT &node, std::vector<EdgeT> *p_in, std::vector<EdgeT> *p_out,
                     EdgeT (*func)(const NodeT &, const std::vector<EdgeT> &, size_t));
-  void LocalModelCheck(bool with_local);
+  /*! \brief fixes (first call) or checks whether checkpoints carry a local model, and sets
+   *  up the replica store: HBM for device local tensors, host memory otherwise */
+  void LocalModelCheck(const Serializable *local_model);
 
   // ---- bootstrap cache (ops issued before LoadCheckPoint)
   int SetBootstrapCache(const std::string &key, const void *buf, size_t nbytes);
@@ -229,8 +250,7 @@ class EngineRobust : public EngineBase {
   ResultLog resbuf_, cachebuf_, lookupbuf_;
   std::string global_checkpoint_;
   const Serializable *global_lazycheck_{nullptr};
-  std::vector<size_t> local_rptr_[2];
-  std::string local_chkpt_[2];
+  LocalReplicas local_;
   // watchdog
   TimeoutHandler timeout_handler_{nullptr};
   std::thread watchdog_;

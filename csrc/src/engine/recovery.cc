@@ -9,10 +9,10 @@
  *  - TryDecideRouting: two tree message-passing rounds (nearest holder by hop count, then the
  *    set of edges that must carry data) -> TryRecoverData streams the bytes along that route,
  *    relaying through bounded staging rings on pass-through nodes;
- *  - local (per-rank) checkpoints are replicated to the next num_local_replica ring successors
- *    and recovered with one backward and one forward ring pass.
- * HBM-resident results are broadcast on the device plane by one holder when every rank can
- * take part (one xGMI hop), otherwise staged through host memory on the ranks of the route.
+ *  - local (per-rank) checkpoints: engine/local_recovery.cc.
+ * HBM-resident results and device checkpoints reach each requester by a device copy from one
+ * holder (one xGMI hop; ranks that neither hold nor request move nothing) when every rank has a
+ * device plane, otherwise they are staged through host memory on the ranks of the route.
  */
 #include <algorithm>
 #include <chrono>
@@ -296,11 +296,9 @@ Status EngineRobust::TryRecoverData(RecoverType role, void *buf_, size_t size, i
 Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, bool requester) {
   if (static_cast<uint32_t>(seqno) == ActionSummary::kLocalCheckAck) return Status::kSuccess;
   if (static_cast<uint32_t>(seqno) == ActionSummary::kLocalCheckPoint) {
-    const int nv = !local_chkpt_version_;
-    const int nlocal = std::max(static_cast<int>(local_rptr_[nv].size()) - 1, 0);
-    utils::Assert(nlocal == 1 || nlocal == num_local_replica_ + 1,
-                  "TryGetResult: local checkpoint state");
-    return TryRecoverLocalState(&local_rptr_[nv], &local_chkpt_[nv]);
+    // some ranks finished the local checkin of the new version, others did not: fill the
+    // missing replicas of the new version from the ranks that hold them
+    return TryRecoverLocalState(!local_chkpt_version_);
   }
   trace::Scope ts("replay", rank_, version_number_, seqno, size, 0);
   RecoverType role;
@@ -334,25 +332,46 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
                  data_size, size);
   }
   if (device_replay_) {
-    // one hop on the xGMI mesh: when every rank can take part on the device and a holder keeps
-    // the result in HBM, the lowest such holder broadcasts it (direct transport or RCCL)
-    // instead of streaming it through host memory along the TCP tree.  Every rank runs this
-    // agreement round (a rank without a device plane votes no).
-    int v[2];
-    v[0] = dev_ == nullptr ? 0 : (role == kPassData ? 1 : (data_dev ? 1 : 0));
-    v[1] = role == kHaveData && data_dev ? rank_ : std::numeric_limits<int>::max();
-    s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+    // one hop on the xGMI mesh: when every rank has a device plane and the result sits in HBM
+    // on a holder and is wanted in HBM by the requesters, each requester gets it by a device
+    // copy from one holder (holders taken in turn), instead of streaming it through host
+    // memory along the TCP tree.  Ranks that neither hold nor request move no bytes.
+    std::vector<int> code;
+    const int mine = (dev_ != nullptr && (role == kPassData || data_dev) ? kReplayCapable : 0) |
+                     (role == kHaveData ? kReplayHolder : 0) |
+                     (role == kRequestData ? kReplayRequester : 0);
+    s = GatherCodes(mine, &code);
     if (s != Status::kSuccess) return s;
-    if (v[0] == 1 && v[1] != std::numeric_limits<int>::max()) {
+    std::vector<int> holders, requesters;
+    bool capable = true;
+    for (int r = 0; r < static_cast<int>(code.size()); ++r) {
+      capable = capable && (code[r] & kReplayCapable) != 0;
+      if (code[r] & kReplayHolder) holders.push_back(r);
+      if (code[r] & kReplayRequester) requesters.push_back(r);
+    }
+    if (capable && !holders.empty()) {
+      std::vector<device::ExchangeItem> plan;
+      for (size_t i = 0; i < requesters.size(); ++i) {
+        device::ExchangeItem x;
+        x.src = holders[i % holders.size()];
+        x.dst = requesters[i];
+        x.key = 0;
+        x.bytes = data_size;
+        x.src_ptr = x.src == rank_ ? data : nullptr;
+        x.dst_ptr = x.dst == rank_ ? data : nullptr;
+        plan.push_back(x);
+      }
       device::DeviceGuard dg(dev_->device());
       s = EnsureDeviceComm();
       if (s != Status::kSuccess) return s;
-      const int root = v[1];
-      void *buf = role == kRequestData || rank_ == root ? data : dev_->Scratch(data_size, 2);
+      size_t got = 0;
       dev_->EnterFromUser();
-      s = dev_->Broadcast(buf, data_size, root, MakeProbe());
+      s = dev_->Exchange(plan, &got);
       if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
-      if (s == Status::kSuccess) stats_.n_device_replays += 1;
+      if (s == Status::kSuccess) {
+        stats_.bytes_replay_in += static_cast<double>(got);
+        if (role == kRequestData) stats_.n_device_replays += 1;
+      }
       return s;
     }
   }
@@ -378,15 +397,10 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
   const RecoverType role = requester ? kRequestData : kHaveData;
   Status s;
   if (num_local_replica_ != 0) {
-    if (requester) {
-      local_rptr_[local_chkpt_version_].clear();
-      local_chkpt_[local_chkpt_version_].clear();
-    }
-    s = TryRecoverLocalState(&local_rptr_[local_chkpt_version_],
-                             &local_chkpt_[local_chkpt_version_]);
+    if (requester) local_.Clear(local_chkpt_version_);
+    s = TryRecoverLocalState(local_chkpt_version_);
     if (s != Status::kSuccess) return s;
-    const int nlocal =
-        std::max(static_cast<int>(local_rptr_[local_chkpt_version_].size()) - 1, 0);
+    const int nlocal = local_.Count(local_chkpt_version_);
     // 1: complete, 2: nothing, 4: partial; any partial node fails the load
     unsigned state = nlocal == num_local_replica_ + 1 ? 1u : (nlocal == 0 ? 2u : 4u);
     s = host_->TreeAllreduce(&state, sizeof(state), 1,
@@ -418,21 +432,30 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
 }
 
 Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
-  // A device checkpoint (HBM snapshot) on the holders and an HBM loader on the requester: the
-  // lowest holder broadcasts the header over the TCP tree and every buffer on the device plane
-  // (one xGMI hop) instead of serialising the model through host memory.  Every rank runs the
-  // agreement round; kAborted (with no side effect) means "take the TCP route".
+  // A device checkpoint (HBM snapshot) on the holders and an HBM loader on the requesters: the
+  // lowest holder broadcasts the small header over the TCP tree, and every requester copies
+  // the buffers from one holder's snapshot (one xGMI hop, holders taken in turn) instead of
+  // serialising the model through host memory; the other ranks move no payload.  Every rank
+  // runs the agreement round; kAborted (with no side effect) means "take the TCP route".
   const bool holder_dev = role == kHaveData && global_lazycheck_ != nullptr && dev_ckpt_ &&
                           dev_ckpt_->IsSnapshot(global_lazycheck_);
   const bool req_dev = role == kRequestData && dev_ckpt_ && dev_ckpt_->loader_active();
-  int v[2];
-  v[0] = dev_ != nullptr && (role == kRequestData ? req_dev : holder_dev) ? 1 : 0;
-  v[1] = holder_dev ? rank_ : std::numeric_limits<int>::max();
-  Status s = host_->TreeAllreduce(v, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+  std::vector<int> code;
+  const int mine =
+      (dev_ != nullptr && (role == kRequestData ? req_dev : true) ? kReplayCapable : 0) |
+      (holder_dev ? kReplayHolder : 0) | (role == kRequestData ? kReplayRequester : 0);
+  Status s = GatherCodes(mine, &code);
   if (s != Status::kSuccess) return s;
-  if (v[0] != 1 || v[1] == std::numeric_limits<int>::max()) return Status::kAborted;
+  std::vector<int> holders, requesters;
+  bool capable = true;
+  for (int r = 0; r < static_cast<int>(code.size()); ++r) {
+    capable = capable && (code[r] & kReplayCapable) != 0;
+    if (code[r] & kReplayHolder) holders.push_back(r);
+    if (code[r] & kReplayRequester) requesters.push_back(r);
+  }
+  if (!capable || holders.empty()) return Status::kAborted;
   device::DeviceGuard dg(dev_->device());
-  const int root = v[1];
+  const int root = holders[0];
   std::string hdr;
   if (rank_ == root) {
     utils::MemoryBufferStream fs(&hdr);
@@ -461,30 +484,51 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
                  "device checkpoint holds %llu buffers, %zu given",
                  static_cast<unsigned long long>(n), dev_ckpt_->loader_targets().size());
   }
+  // every requester reads every buffer from one holder's snapshot (holders taken in turn)
+  std::vector<device::ExchangeItem> plan;
+  for (size_t q = 0; q < requesters.size(); ++q) {
+    const int src = holders[q % holders.size()];
+    for (size_t i = 0; i < n; ++i) {
+      if (sizes[i] == 0) continue;
+      device::ExchangeItem x;
+      x.src = src;
+      x.dst = requesters[q];
+      x.key = static_cast<int>(i);
+      x.bytes = sizes[i];
+      x.src_ptr = src == rank_ ? dev_ckpt_->SnapshotBuffer(global_lazycheck_, i) : nullptr;
+      x.dst_ptr = nullptr;
+      if (x.dst == rank_) {
+        utils::Check(dev_ckpt_->loader_sizes()[i] == sizes[i],
+                     "device checkpoint buffer %zu: %llu bytes stored, %zu given", i,
+                     static_cast<unsigned long long>(sizes[i]), dev_ckpt_->loader_sizes()[i]);
+        x.dst_ptr = dev_ckpt_->loader_targets()[i];
+      }
+      plan.push_back(x);
+    }
+  }
   s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
-  for (size_t i = 0; i < n; ++i) {
-    if (sizes[i] == 0) continue;
-    void *buf;
-    if (role == kRequestData) {
-      utils::Check(dev_ckpt_->loader_sizes()[i] == sizes[i],
-                   "device checkpoint buffer %zu: %llu bytes stored, %zu given", i,
-                   static_cast<unsigned long long>(sizes[i]), dev_ckpt_->loader_sizes()[i]);
-      buf = dev_ckpt_->loader_targets()[i];
-    } else {
-      buf = dev_ckpt_->SnapshotBuffer(global_lazycheck_, i);  // same bytes on every holder
-    }
-    dev_->EnterFromUser();
-    s = dev_->Broadcast(buf, sizes[i], root, MakeProbe());
-    if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
-    if (s != Status::kSuccess) return s;
-  }
+  size_t got = 0;
+  dev_->EnterFromUser();
+  s = dev_->Exchange(plan, &got);
+  if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+  if (s != Status::kSuccess) return s;
+  stats_.bytes_ckpt_in += static_cast<double>(got);
   if (role == kRequestData) {
     global_checkpoint_ = hdr;  // version + header; the payload is already in the targets
     dev_ckpt_->MarkPayloadDelivered();
   }
   stats_.n_device_ckpt_loads += 1;
   return Status::kSuccess;
+}
+
+Status EngineRobust::GatherCodes(int mine, std::vector<int> *all) {
+  const int n = GetWorldSize();
+  all->assign(n, 0);
+  (*all)[rank_] = mine;
+  if (n == 1) return Status::kSuccess;
+  return host_->RingAllgather(all->data(), sizeof(int) * n, sizeof(int) * rank_,
+                              sizeof(int) * (rank_ + 1), sizeof(int));
 }
 
 Status EngineRobust::TryRestoreCache(bool requester, int min_seq, int max_seq) {
@@ -525,119 +569,6 @@ Status EngineRobust::TryRestoreCache(bool requester, int min_seq, int max_seq) {
     if (requester) cur_cache_seq_ += 1;
   }
   return Status::kSuccess;
-}
-
-// ------------------------------------------------------------------ local state on the ring
-Status EngineRobust::TryRecoverLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt) {
-  if (num_local_replica_ == 0) return Status::kSuccess;
-  std::vector<size_t> &rptr = *p_rptr;
-  std::string &chkpt = *p_chkpt;
-  if (rptr.empty()) {
-    rptr.push_back(0);
-    utils::Assert(chkpt.empty(), "local checkpoint storage inconsistent");
-  }
-  const int n = num_local_replica_;
-  net::PeerLink *next = topo_.ring_next, *prev = topo_.ring_prev;
-  // Slot k of a node holds the local model of the node k hops back on the ring
-  // (slot 0 = own).  Backward pass (next -> prev): a node refills its low slots from its
-  // successors, which hold its model one slot further.  Forward pass (prev -> next): it then
-  // refills the remaining high slots from its predecessor.
-  {
-    const int nlocal = static_cast<int>(rptr.size()) - 1;
-    utils::Assert(nlocal <= n + 1, "too many local replicas");
-    std::vector<int> msg_back(n + 1);
-    msg_back[0] = nlocal;  // -> msg_back[i] = slot count of the i-th successor
-    Status s = host_->RingPass(msg_back.data(), sizeof(int), (n + 1) * sizeof(int), 0,
-                               n * sizeof(int), next, prev);
-    if (s != Status::kSuccess) return s;
-    int msg_fwd[2] = {nlocal, 0};  // -> msg_fwd[1] = slot count of the predecessor
-    s = host_->RingPass(msg_fwd, sizeof(int), 2 * sizeof(int), 0, sizeof(int), prev, next);
-    if (s != Status::kSuccess) return s;
-    int nread_end = nlocal;
-    for (int i = 1; i <= n; ++i) nread_end = std::max(nread_end, msg_back[i] - i);
-    const int nwrite_start = std::min(msg_fwd[1] + 1, nread_end);
-    std::vector<size_t> sizes(nread_end);
-    for (int i = 0; i < nlocal; ++i) sizes[i] = rptr[i + 1] - rptr[i];
-    s = host_->RingPass(sizes.data(), nlocal * sizeof(size_t), nread_end * sizeof(size_t),
-                        nwrite_start * sizeof(size_t), nread_end * sizeof(size_t), next, prev);
-    if (s != Status::kSuccess) return s;
-    rptr.resize(nread_end + 1);
-    for (int i = nlocal; i < nread_end; ++i) rptr[i + 1] = rptr[i] + sizes[i];
-    chkpt.resize(rptr.back());
-    s = host_->RingPass(BeginPtr(chkpt), rptr[nlocal], rptr[nread_end], rptr[nwrite_start],
-                        rptr[nread_end], next, prev);
-    if (s != Status::kSuccess) {
-      rptr.resize(nlocal + 1);
-      chkpt.resize(rptr.back());
-      return s;
-    }
-  }
-  {
-    const int nlocal = static_cast<int>(rptr.size()) - 1;
-    utils::Assert(nlocal <= n + 1, "too many local replicas");
-    std::vector<int> msg_fwd(n + 1);
-    msg_fwd[0] = nlocal;  // -> msg_fwd[i] = slot count of the i-th predecessor
-    Status s = host_->RingPass(msg_fwd.data(), sizeof(int), (n + 1) * sizeof(int), 0,
-                               n * sizeof(int), prev, next);
-    if (s != Status::kSuccess) return s;
-    int msg_back[2] = {nlocal, 0};  // -> msg_back[1] = slot count of the successor
-    s = host_->RingPass(msg_back, sizeof(int), 2 * sizeof(int), 0, sizeof(int), next, prev);
-    if (s != Status::kSuccess) return s;
-    int nread_end = nlocal, nwrite_end = 1;
-    if (nlocal != 0) {
-      // slot i arrives from the predecessor chain as long as every hop up to i holds data
-      for (int i = 1; i <= n; ++i) {
-        if (msg_fwd[i] == 0) break;
-        nread_end = std::max(nread_end, i + 1);
-        nwrite_end = i + 1;
-      }
-      if (nwrite_end > n) nwrite_end = n;
-    } else {
-      nread_end = 0;
-      nwrite_end = 0;
-    }
-    int nwrite_start = std::min(msg_back[1] - 1, nwrite_end);
-    if (nwrite_start < 0) nwrite_start = nwrite_end = 0;  // successor lost its own state
-    std::vector<size_t> sizes(nread_end);
-    for (int i = 0; i < nlocal; ++i) sizes[i] = rptr[i + 1] - rptr[i];
-    s = host_->RingPass(sizes.data(), nlocal * sizeof(size_t), nread_end * sizeof(size_t),
-                        nwrite_start * sizeof(size_t), nwrite_end * sizeof(size_t), prev, next);
-    if (s != Status::kSuccess) return s;
-    rptr.resize(nread_end + 1);
-    for (int i = nlocal; i < nread_end; ++i) rptr[i + 1] = rptr[i] + sizes[i];
-    chkpt.resize(rptr.back());
-    s = host_->RingPass(BeginPtr(chkpt), rptr[nlocal], rptr[nread_end], rptr[nwrite_start],
-                        rptr[nwrite_end], prev, next);
-    if (s != Status::kSuccess) {
-      rptr.resize(nlocal + 1);
-      chkpt.resize(rptr.back());
-      return s;
-    }
-  }
-  return Status::kSuccess;
-}
-
-Status EngineRobust::TryCheckinLocalState(std::vector<size_t> *p_rptr, std::string *p_chkpt) {
-  if (num_local_replica_ == 0) return Status::kSuccess;
-  std::vector<size_t> &rptr = *p_rptr;
-  std::string &chkpt = *p_chkpt;
-  utils::Assert(rptr.size() == 2, "TryCheckinLocalState needs exactly the own state");
-  const int n = num_local_replica_;
-  net::PeerLink *next = topo_.ring_next, *prev = topo_.ring_prev;
-  std::vector<size_t> sizes(n + 1);
-  sizes[0] = rptr[1] - rptr[0];
-  Status s = host_->RingPass(sizes.data(), sizeof(size_t), (n + 1) * sizeof(size_t), 0,
-                             n * sizeof(size_t), prev, next);
-  if (s != Status::kSuccess) return s;
-  rptr.resize(n + 2);
-  for (int i = 1; i <= n; ++i) rptr[i + 1] = rptr[i] + sizes[i];
-  chkpt.resize(rptr.back());
-  s = host_->RingPass(BeginPtr(chkpt), rptr[1], rptr[n + 1], rptr[0], rptr[n], prev, next);
-  if (s != Status::kSuccess) {
-    rptr.resize(2);
-    chkpt.resize(rptr.back());
-  }
-  return s;
 }
 
 // ------------------------------------------------------------------ consensus state machine

@@ -76,6 +76,15 @@ def _declare(d: ctypes.CDLL) -> None:
                                            ctypes.POINTER(c_size_t),
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_char)),
                                            ctypes.POINTER(c_ulong)]),
+        "RabitDevCheckPointEx": (None, [c_int, ctypes.POINTER(c_void_p),
+                                        ctypes.POINTER(c_size_t), c_char_p, c_ulong, c_int,
+                                        ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
+        "RabitDevLoadCheckPointEx": (c_int, [c_int, ctypes.POINTER(c_void_p),
+                                             ctypes.POINTER(c_size_t),
+                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_char)),
+                                             ctypes.POINTER(c_ulong), c_int,
+                                             ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
+        "RabitDevSetTransport": (c_int, [c_int, c_int]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),
         "RabitTraceDump": (c_int, [c_char_p]),

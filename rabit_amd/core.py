@@ -317,38 +317,54 @@ def lazy_checkpoint(global_model: Any):
 
 
 def _tensor_list(tensors):
+    if tensors is None:
+        tensors = []
     items = list(tensors.values()) if isinstance(tensors, dict) else list(tensors)
     for t in items:
         if not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
             raise TypeError("device checkpoints take contiguous HBM (cuda) tensors")
     n = len(items)
-    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in items])
-    sizes = (ctypes.c_size_t * n)(*[t.numel() * t.element_size() for t in items])
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in items])
+    sizes = (ctypes.c_size_t * max(n, 1))(*[t.numel() * t.element_size() for t in items])
     return items, n, ptrs, sizes
 
 
-def checkpoint_tensors(tensors, meta: Any = None):
+def checkpoint_tensors(tensors, meta: Any = None, local=None):
     """Checkpoint HBM tensors (dict or list) plus a picklable `meta`: HBM snapshot with the
     gfx950 copy kernel and an asynchronous pinned-host mirror on a side stream; the bytes are
-    only serialised if a recovering peer asks for them.  Version number += 1."""
+    only serialised if a recovering peer asks for them.  `local`: this rank's own tensors
+    (its local model): kept in HBM together with the local models of its rabit_local_replica
+    ring predecessors and replicated to its successors over xGMI, never through host memory.
+    Version number += 1."""
     _check_init()
     items, n, ptrs, sizes = _tensor_list(tensors)
-    if items:
-        _sync_stream_for(items[0])
+    litems, nl, lptrs, lsizes = _tensor_list(local)
+    if items or litems:
+        _sync_stream_for((items or litems)[0])
     m = pickle.dumps(meta)
-    _LIB.RabitDevCheckPoint(n, ptrs, sizes, m, len(m))
+    if local is None:
+        _LIB.RabitDevCheckPoint(n, ptrs, sizes, m, len(m))
+    else:
+        _LIB.RabitDevCheckPointEx(n, ptrs, sizes, m, len(m), nl, lptrs, lsizes)
 
 
-def load_checkpoint_tensors(tensors):
+def load_checkpoint_tensors(tensors, local=None):
     """Fill HBM tensors (same order/shapes as checkpointed) from the latest device
-    checkpoint; returns (version, meta), version 0 = nothing checkpointed (tensors untouched)."""
+    checkpoint, and this rank's `local` tensors from the replicated local checkpoint;
+    returns (version, meta), version 0 = nothing checkpointed (tensors untouched)."""
     _check_init()
     items, n, ptrs, sizes = _tensor_list(tensors)
-    if items:
-        _sync_stream_for(items[0])
+    litems, nl, lptrs, lsizes = _tensor_list(local)
+    if items or litems:
+        _sync_stream_for((items or litems)[0])
     mptr = ctypes.POINTER(ctypes.c_char)()
     mlen = ctypes.c_ulong()
-    version = _LIB.RabitDevLoadCheckPoint(n, ptrs, sizes, ctypes.byref(mptr), ctypes.byref(mlen))
+    if local is None:
+        version = _LIB.RabitDevLoadCheckPoint(n, ptrs, sizes, ctypes.byref(mptr),
+                                              ctypes.byref(mlen))
+    else:
+        version = _LIB.RabitDevLoadCheckPointEx(n, ptrs, sizes, ctypes.byref(mptr),
+                                                ctypes.byref(mlen), nl, lptrs, lsizes)
     if version <= 0:
         return (version, None)
     return (version, _load_model(mptr, mlen.value))
@@ -380,6 +396,21 @@ def dump_trace(path: str) -> int:
     returns the number of spans."""
     _check_init()
     return _LIB.RabitTraceDump(path.encode())
+
+
+TRANSPORT_AUTO = -1
+TRANSPORT_RCCL = 0
+TRANSPORT_DIRECT = 1
+
+
+def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str] = None) -> bool:
+    """Route this rank's device collectives over one transport (benchmarks / diagnosis):
+    TRANSPORT_AUTO (the calibrated choice), TRANSPORT_RCCL or TRANSPORT_DIRECT, and pick the
+    direct reduce-scatter variant ("pull" / "push").  Every rank must make the same call between
+    the same collectives.  False when that transport is not up on this rank."""
+    _check_init()
+    mode = {None: 0, "pull": 1, "push": 2}[direct_mode]
+    return _LIB.RabitDevSetTransport(int(which), mode) == 0
 
 
 def last_error() -> str:

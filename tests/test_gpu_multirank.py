@@ -117,6 +117,13 @@ def test_bench_torchrun_shared_gpu(n):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["transport"]["direct"] == 1, rec
+    assert rec["result_check"], rec
+    # every available transport x input variant ran and matched the host fp64 reference
+    ran = [v for v in rec["variants"] if v["available"]]
+    assert {(v["transport"], v["input"]) for v in ran} >= {
+        ("direct-pull", "torch"), ("direct-push", "torch"), ("direct-pull", "symmetric"),
+        ("direct-push", "symmetric")}, rec["variants"]
+    assert all(v["check"] and v["t_us"] > 0 for v in ran), rec["variants"]
 
 
 @pytest.mark.parametrize("mode", ["pull", "push"])
@@ -129,3 +136,54 @@ def test_direct_half_precision(mode):
     assert rc == 0, out[-5000:]
     assert out.count("HALF OK") == 3, out[-3000:]
 
+
+
+# the LOCAL kill matrix of tests/test_recovery.py, scaled to 5 ranks: deaths at the checkpoint
+# call (seq 1), repeated deaths of one rank, and a death inside the allreduce (seq 0)
+LOCAL_KILLS = ["mock=0,0,1,0", "mock=1,1,1,0", "mock=0,1,1,0", "mock=3,1,1,0", "mock=1,1,1,1",
+               "mock=2,2,0,0"]
+
+
+@pytest.mark.parametrize("extra", [[], ["force_local=1"]])
+def test_device_local_checkpoint_recovery(extra):
+    """local tensors (per-rank state) checkpointed in HBM and replicated to the ring successors
+    by device copies; restarted ranks get them back bit for bit (force_local=1: the global
+    tensors travel as local state too)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_local.py", 5, LOCAL_KILLS + extra, attempts=4, timeout=300)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVLOCAL OK") == 5, out[-3000:]
+    assert "local tensors intact" in out, out[-3000:]
+    import re
+    got = [int(x) for x in re.findall(r"DEVLOCAL OK bytes_local_in=(\d+)", out)]
+    assert all(g > 0 for g in got), got
+
+
+@pytest.mark.parametrize("mode", ["pull", "push"])
+def test_device_hang_detected_and_recovered(mode):
+    """mock_dev_hang: rank 1 stays alive but its GPU stream wedges right before a device
+    allreduce.  The survivors' barriers give up, they abort and re-link; rank 1 finds its own
+    stream still stuck after the abort and exits for a restart; the job finishes with the
+    closed-form model."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_ft.py", 3, ["mock_dev_hang=1,1,0,0", "rabit_device_drain_timeout_sec=5",
+                                       "rabit_device_direct_mode=" + mode], attempts=3, timeout=240)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVFT OK") == 3, out[-3000:]
+    assert "Hit Mock Device Hang" in out and "device stream wedged" in out, out[-3000:]
+    assert "resumed at version" in out, out[-3000:]
+
+
+def test_forced_rccl_on_shared_gpu_fails_fast():
+    """rabit_device_algo=rccl with ranks sharing one GPU: RCCL refuses that layout, so the job
+    must stop at once with a clear message instead of hanging in ncclCommInitRank"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import time
+    t0 = time.time()
+    rc, out = _run("device_multi.py", 2, ["rabit_device_algo=rccl"], attempts=1, timeout=120)
+    assert rc != 0
+    assert "no device transport" in out and "rabit_device_algo=rccl" in out, out[-3000:]
+    assert time.time() - t0 < 90
