@@ -30,7 +30,7 @@ CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc 
              csrc/src/engine/recovery.cc csrc/src/engine/local_replicas.cc csrc/src/engine/local_recovery.cc \
              csrc/src/capi/c_api.cc
 CORE_OBJS := $(patsubst csrc/src/%.cc,$(OBJ)/%.o,$(CORE_SRCS))
-KERN_OBJ  := $(OBJ)/device/kernels.o $(OBJ)/device/peer_kernels.o
+KERN_OBJ  := $(OBJ)/device/kernels.o $(OBJ)/device/peer_kernels.o $(OBJ)/device/fused_allreduce.o
 HEADERS   := $(shell find csrc -name '*.h')
 
 FLAVOURS  := rabit rabit_base rabit_mock rabit_empty

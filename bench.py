@@ -8,8 +8,9 @@ measured faster) written straight into the HBM result log and the user tensor.  
 skipped.
 
 At N > 1 the run also times every transport the job has up, side by side, on torch-allocated
-and on symmetric-heap inputs (RCCL, direct pull, direct push), each first checked bit for bit
-against a host fp64 reference.  At N = 1 no byte moves between ranks: the step is the robust
+and on symmetric-heap inputs (RCCL; direct pull and push, each as one fused kernel per chunk and
+in the classic 5-launch form), each first checked bit for bit against a host fp64 reference.
+At N = 1 no byte moves between ranks: the step is the robust
 engine's bookkeeping plus its HBM result-log copy (rabit_world1_fastpath=0), reported as such
 (`collective: false`); busbw is 0 by definition.
 
@@ -206,12 +207,16 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps):
         bufs.append(("symmetric", rabit.symmetric_empty(n, torch.float32)))
     except MemoryError:
         pass
-    variants = [("rccl", rabit.TRANSPORT_RCCL, None), ("direct-pull", rabit.TRANSPORT_DIRECT, "pull"),
-                ("direct-push", rabit.TRANSPORT_DIRECT, "push")]
+    variants = [("rccl", rabit.TRANSPORT_RCCL, None, None)]
+    for mode in ("pull", "push"):
+        for fused in (False, True):
+            variants.append(("direct-%s-%s" % (mode, "fused" if fused else "classic"),
+                             rabit.TRANSPORT_DIRECT, mode, fused))
+    st0 = rabit.stats()
     for input_name, x in bufs:
-        for name, which, mode in variants:
+        for name, which, mode, fused in variants:
             phase("variant %s/%s" % (name, input_name))
-            up = rabit.set_device_transport(which, mode)
+            up = rabit.set_device_transport(which, mode, fused)
             # the same choice on every rank, or none
             up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
             rec = {"transport": name, "input": input_name, "available": bool(up)}
@@ -226,11 +231,11 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps):
                 rec["busbw_GBps"] = round(n * 4 / t / 1e9 * 2 * (world - 1) / world, 2)
                 rabit.checkpoint(None)  # bounded result log
             out.append(rec)
+    # back to the calibrated choice of transport and direct form
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
-    st = rabit.stats()
-    if st.get("device_direct"):
-        # back to the calibrated pull/push choice
-        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st.get("direct_push") else "pull")
+    if st0.get("device_direct"):
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+                                   bool(st0.get("direct_fused")))
     return out
 
 
@@ -356,6 +361,11 @@ def main():
                       "calibration_us": st.get("calib_us"),
                       "direct_variant": "push" if st.get("direct_push") else "pull",
                       "calibration_push_us": st.get("calib_push_us"),
+                      "calibration_forms_us": dict(zip(
+                          ["pull-classic", "pull-fused", "push-classic", "push-fused"],
+                          st.get("calib_forms_us", []))),
+                      "direct_fused": bool(st.get("direct_fused", 0)),
+                      "fused_chunks": st.get("fused_chunks", 0),
                       "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),
                       "peer_links": st.get("peer_links")},
         "variants": variants,

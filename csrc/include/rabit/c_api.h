@@ -107,6 +107,13 @@ RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes);
  *        call between the same collectives.  -1 when the transport is not up.
  */
 RABIT_DLL int RabitDevSetTransport(int which, int direct_mode);
+/*!
+ * \brief form of the direct transport's two-shot allreduce: 1 one fused kernel per chunk
+ *        (per-tile hand-offs), 0 the classic stage/barrier/reduce/barrier/gather launches.
+ *        Every rank must make the same call between the same collectives.
+ * \return 0, or -1 when the direct transport is not up
+ */
+RABIT_DLL int RabitDevSetFused(int fused);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

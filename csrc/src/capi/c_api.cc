@@ -283,6 +283,13 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode) {
   return 0;
 }
 
+RABIT_DLL int RabitDevSetFused(int fused) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr || !e->device_plane()->has_peers()) return -1;
+  e->device_plane()->SetFused(fused != 0);
+  return 0;
+}
+
 RABIT_DLL const char *RabitGetLastError() { return g_last_error.c_str(); }
 
 RABIT_DLL const char *RabitGetStats() {

@@ -78,7 +78,13 @@ std::atomic<int *> g_hang_release{nullptr};
 
 // ------------------------------------------------------------------ arena
 DeviceArena::~DeviceArena() {
-  for (auto &c : chunks_) (void)hipFree(c.base);
+  for (auto &c : chunks_) {
+    if (pinned_) {
+      (void)hipHostFree(c.base);
+    } else {
+      (void)hipFree(c.base);
+    }
+  }
 }
 
 void *DeviceArena::Alloc(size_t bytes) {
@@ -98,7 +104,9 @@ void *DeviceArena::Alloc(size_t bytes) {
   c.size = std::max(need, chunk_);
   c.used = need;
   void *base = nullptr;
-  if (hipMalloc(&base, c.size) != hipSuccess) {
+  const hipError_t e =
+      pinned_ ? hipHostMalloc(&base, c.size, hipHostMallocDefault) : hipMalloc(&base, c.size);
+  if (e != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
@@ -164,6 +172,7 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   CheckHip(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
   CheckHip(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
   arena_.Configure(cfg.arena_chunk, cfg.arena_cap);
+  spill_.Configure(std::min<size_t>(cfg.arena_chunk, 64u << 20), cfg.spill_cap, true);
   if (cfg.sym_heap > 0) {
     // symmetric heap: uncached like the stage buffers (peers read it over xGMI in place)
     heap_.bytes = (cfg.sym_heap + (1u << 16) - 1) & ~static_cast<size_t>((1u << 16) - 1);
@@ -379,6 +388,9 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     if (cfg_.phase_timing) peers_->EnableTiming();
     peers_->set_oneshot_max(cfg_.oneshot_max);
     peers_->set_push(cfg_.direct_mode == 2);
+    peers_->set_fused(cfg_.fused_mode == 1);  // auto: classic until the calibration decides
+    peers_->set_fused_grid(cfg_.fused_grid);
+    peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();

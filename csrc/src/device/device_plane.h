@@ -42,7 +42,10 @@ struct DeviceConfig {
   double op_timeout_sec{-1};           // deadline of a device op: < 0 auto (size-scaled), 0 none
   double drain_timeout_sec{30};        // after an abort, the stream must drain within this
   size_t arena_chunk{256u << 20};      // result-log arena growth step
-  size_t arena_cap{size_t(64) << 30};  // beyond this the result log spills to pinned host memory
+  size_t arena_cap{size_t(64) << 30};  // HBM result-log cap; beyond it (or when hipMalloc fails)
+                                       // results spill to pinned host memory
+  size_t spill_cap{size_t(1) << 40};   // pinned host bytes the result log may spill (0: no spill,
+                                       // a full HBM log is then an error)
   int spin_us{5000};                   // busy-poll window before sleeping while waiting
   int algo{0};                         // 0 auto, 1 RCCL only, 2 direct (IPC peer memory) only
   size_t peer_stage{256u << 20};       // direct transport: bytes per stage buffer (x2 per rank)
@@ -53,6 +56,10 @@ struct DeviceConfig {
   size_t sym_heap{0};                  // bytes of the symmetric (IPC-exported) heap, 0: none
   size_t oneshot_max{256u << 10};      // direct allreduce: one-shot up to this many bytes
   int direct_mode{0};                  // direct reduce-scatter: 0 calibrated, 1 pull, 2 push
+  int fused_mode{2};                   // direct two-shot chunks as one fused kernel: 0 never,
+                                       // 1 always, 2 as the calibration finds faster
+  int fused_grid{0};                   // workgroups of a fused launch (0: automatic)
+  size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
 };
 
 /*! \brief exit status of a rank whose own device stream stayed wedged after an abort (the
@@ -62,14 +69,17 @@ constexpr int kDeviceHangExitCode = 251;
 inline double AutoOpDeadline(size_t bytes) { return 60.0 + static_cast<double>(bytes) * 1e-9; }
 
 /*! \brief HBM arena for the robust engine's result log and checkpoints (bump allocator over
- *  chunks; Reset() keeps the chunks so steady-state iterations never call hipMalloc) */
+ *  chunks; Reset() keeps the chunks so steady-state iterations never call hipMalloc).  A pinned
+ *  arena holds page-locked host memory instead (the result log's spill space past its HBM cap) */
 class DeviceArena {
  public:
   ~DeviceArena();
-  void Configure(size_t chunk, size_t cap) {
+  void Configure(size_t chunk, size_t cap, bool pinned = false) {
     chunk_ = chunk;
     cap_ = cap;
+    pinned_ = pinned;
   }
+  bool pinned() const { return pinned_; }
   /*! \brief 256-byte aligned slot, nullptr when over the cap or out of memory */
   void *Alloc(size_t bytes);
   /*! \brief give back the most recent allocation (ResultLog::DropLast) */
@@ -86,6 +96,7 @@ class DeviceArena {
   std::vector<Chunk> chunks_;
   size_t cur_{0};
   size_t chunk_{256u << 20}, cap_{size_t(64) << 30};
+  bool pinned_{false};
 };
 
 /*!
@@ -128,6 +139,10 @@ class DevicePlane {
   void SetUserStream(hipStream_t s);
   hipStream_t stream() const { return stream_; }
   DeviceArena *arena() { return &arena_; }
+  /*! \brief pinned host arena the result log spills to (nullptr: spilling disabled) */
+  DeviceArena *spill_arena() { return cfg_.spill_cap != 0 ? &spill_ : nullptr; }
+  /*! \brief scratch slot staging spilled results (HBM side of the D2H / H2D copies) */
+  static constexpr int kSpillScratch = 3;
   const DeviceConfig &config() const { return cfg_; }
 
   // ---- communicator lifecycle
@@ -208,6 +223,12 @@ class DevicePlane {
   size_t sym_heap_used() const { return heap_used_; }
   uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
   uint64_t oneshot_ops() const { return peers_ ? peers_->oneshot_ops() : 0; }
+  uint64_t fused_chunks() const { return peers_ ? peers_->fused_chunks() : 0; }
+  void SetFused(bool v) {
+    if (peers_ != nullptr) peers_->set_fused(v);
+  }
+  bool fused() const { return peers_ != nullptr && peers_->fused(); }
+  int fused_grid() const { return peers_ ? peers_->fused_grid() : 0; }
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;
 
@@ -290,6 +311,7 @@ class DevicePlane {
   ncclComm_t comm_{nullptr};
   int nranks_{0}, rank_{0}, epoch_{0};
   DeviceArena arena_;
+  DeviceArena spill_;
   std::unique_ptr<PeerGroup> peers_;
   SymHeapInfo heap_;
   size_t heap_used_{0};
@@ -297,9 +319,10 @@ class DevicePlane {
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};
   size_t pending_bytes_{0};
-  static constexpr int kScratchSlots = 3;  // 0/1: all-to-all path, 2: host-buffer staging
-  void *scratch_[kScratchSlots]{nullptr, nullptr, nullptr};
-  size_t scratch_bytes_[kScratchSlots]{0, 0, 0};
+  // 0/1: all-to-all path, 2: host-buffer staging, 3: spilled results
+  static constexpr int kScratchSlots = 4;
+  void *scratch_[kScratchSlots]{nullptr, nullptr, nullptr, nullptr};
+  size_t scratch_bytes_[kScratchSlots]{0, 0, 0, 0};
   void *pinned_{nullptr};
   size_t pinned_bytes_{0};
   size_t op_bytes_{0};

@@ -29,61 +29,17 @@
 #include <type_traits>
 
 #include "device/kernels.h"
+#include "device/vec_ops.h"
 #include "rabit/internal/half.h"
 
 namespace rabit {
 namespace device {
 namespace {
+using namespace vec;  // NOLINT
 
 constexpr int kBlock = 256;
 
-enum OpCode : int { kOpMax = 0, kOpMin = 1, kOpSum = 2, kOpOr = 3 };
-
-template <typename T, int OP>
-struct Apply;
-template <typename T>
-struct Apply<T, kOpMax> {
-  __device__ __forceinline__ static T f(T a, T b) { return b > a ? b : a; }
-};
-template <typename T>
-struct Apply<T, kOpMin> {
-  __device__ __forceinline__ static T f(T a, T b) { return b < a ? b : a; }
-};
-template <typename T>
-struct Apply<T, kOpSum> {
-  __device__ __forceinline__ static T f(T a, T b) { return a + b; }
-};
-template <typename T>
-struct Apply<T, kOpOr> {
-  __device__ __forceinline__ static T f(T a, T b) { return a | b; }
-};
-
-/*! \brief lane-wise op on the T lanes of two 16-byte vectors */
-template <typename T, int OP>
-__device__ __forceinline__ uint4 Combine(uint4 a, uint4 b) {
-  constexpr int L = 16 / sizeof(T);
-  T x[L], y[L];
-  __builtin_memcpy(x, &a, 16);
-  __builtin_memcpy(y, &b, 16);
-#pragma unroll
-  for (int j = 0; j < L; ++j) x[j] = Apply<T, OP>::f(x[j], y[j]);
-  uint4 r;
-  __builtin_memcpy(&r, x, 16);
-  return r;
-}
-
 inline bool Aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-/*! \brief streaming (nontemporal) 16-byte store: for outputs that are not the buffer just read
- *  (two inputs -> third buffer measured 71 -> 57 us per 128 MiB; neutral for in-place / copy) */
-__device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
-  u32x4_t w = {v.x, v.y, v.z, v.w};
-  // compiler-only barrier: without it a later pass rebuilds this store as <4 x float> and drops
-  // the !nontemporal tag in the multi-source kernel (seen in the LLVM IR of hipcc, ROCm 7.2)
-  asm volatile("" ::: "memory");
-  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
-}
 
 /*! \brief workgroups for a one-shot tile grid over nvec vectors (>= 1) */
 inline unsigned TileGrid(size_t nvec, int unroll) {
@@ -149,32 +105,6 @@ hipError_t Reduce2(void *dst, const void *src, size_t n, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename T>
-__device__ __forceinline__ T PrepApply(T x, int prep, T alpha) {
-  switch (prep) {
-    case kPrepSquare: return x * x;
-    case kPrepScale: return x * alpha;
-    case kPrepAbs:
-      if constexpr (std::is_signed<T>::value || IsHalfType<T>::value) {
-        return x < T(0) ? T(0) - x : x;
-      }
-      return x;
-    default: return x;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ uint4 PrepVec(uint4 v, int prep, T alpha) {
-  constexpr int L = 16 / sizeof(T);
-  T x[L];
-  __builtin_memcpy(x, &v, 16);
-#pragma unroll
-  for (int j = 0; j < L; ++j) x[j] = PrepApply<T>(x[j], prep, alpha);
-  uint4 r;
-  __builtin_memcpy(&r, x, 16);
-  return r;
-}
-
 // ---------------------------------------------------------------- multi-source reduce
 struct SrcList {
   const void *p[kMaxReduceSources];
@@ -193,38 +123,6 @@ __device__ __forceinline__ const void *Src(const SrcList &s, int k) {
 __device__ __forceinline__ bool Guarded(const int *guard) {
   return guard != nullptr &&
          __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-}
-
-/*! \brief op over NSRC 16-byte vectors, then the optional post scale.  16-bit floats are
- *  widened: every element is accumulated over all sources in fp32 and rounded once */
-template <typename T, int OP, int NSRC>
-__device__ __forceinline__ uint4 ReduceVecs(const uint4 *v, double post) {
-  if constexpr (IsHalfType<T>::value) {
-    constexpr int L = 8;
-    T t[L];
-    float acc[L];
-    __builtin_memcpy(t, &v[0], 16);
-#pragma unroll
-    for (int j = 0; j < L; ++j) acc[j] = t[j].f();
-#pragma unroll
-    for (int k = 1; k < NSRC; ++k) {
-      __builtin_memcpy(t, &v[k], 16);
-#pragma unroll
-      for (int j = 0; j < L; ++j) acc[j] = Apply<float, OP>::f(acc[j], t[j].f());
-    }
-    const float ps = static_cast<float>(post);
-#pragma unroll
-    for (int j = 0; j < L; ++j) t[j] = T(post != 0.0 ? acc[j] * ps : acc[j]);
-    uint4 r;
-    __builtin_memcpy(&r, t, 16);
-    return r;
-  } else {
-    uint4 acc = v[0];
-#pragma unroll
-    for (int k = 1; k < NSRC; ++k) acc = Combine<T, OP>(acc, v[k]);
-    if (post != 0.0) acc = PrepVec<T>(acc, kPrepScale, static_cast<T>(post));
-    return acc;
-  }
 }
 
 /*! \brief scalar form of ReduceVecs over nsrc sources (tails, unaligned buffers) */
@@ -431,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void CopyTileKernel(uint4 *__restrict__ dst
  * One 64-bit multiply per 16 bytes keeps it bandwidth-bound; order changes across vectors
  * and within a vector both change s2.
  */
-constexpr int kChecksumGrid = 1024;  // 4 workgroups per CU, tiles walked grid-stride
+constexpr int kChecksumGrid = 2048;  // 8 workgroups per CU, tiles walked grid-stride
 
 __device__ __forceinline__ void BlockSum2(unsigned long long &s1, unsigned long long &s2) {
 #pragma unroll
@@ -456,12 +354,18 @@ __device__ __forceinline__ void BlockSum2(unsigned long long &s1, unsigned long 
   }
 }
 
-/*! \brief pass 1: each workgroup folds its tiles into one (s1, s2) partial (no atomics: 8192
- *  workgroups adding into one word serialise, measured 3.3x slower than this two-pass form) */
+/*!
+ * \brief one launch: each workgroup folds its tiles into one (s1, s2) partial, and the workgroup
+ *        that arrives last (agent-scope counter) adds all partials into out and re-arms the
+ *        counter.  No atomics on the sums themselves (8192 workgroups adding into one word
+ *        serialise, measured 3.3x slower than partials) and no second launch (a dependent
+ *        one-workgroup kernel costs ~4 us, 15 % of a 128 MiB checksum).
+ */
 template <int U>
-__global__ __launch_bounds__(kBlock) void ChecksumPartialKernel(const uint4 *__restrict__ w,
-                                                               size_t nvec,
-                                                               unsigned long long *partial) {
+__global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint4 *__restrict__ w, size_t nvec,
+                                                         unsigned long long *partial,
+                                                         unsigned int *arrived,
+                                                         unsigned long long *out) {
   unsigned long long s1 = 0, s2 = 0;
   const size_t ntile = (nvec + static_cast<size_t>(kBlock) * U - 1) / (kBlock * U);
   for (size_t t = blockIdx.x; t < ntile; t += gridDim.x) {
@@ -482,25 +386,26 @@ __global__ __launch_bounds__(kBlock) void ChecksumPartialKernel(const uint4 *__r
     }
   }
   BlockSum2(s1, s2);
+  __shared__ bool last;
   if (threadIdx.x == 0) {
     partial[2 * blockIdx.x] = s1;
     partial[2 * blockIdx.x + 1] = s2;
+    __threadfence();  // the partial is visible before the arrival is counted
+    last = atomicAdd(arrived, 1u) == gridDim.x - 1;
   }
-}
-
-/*! \brief pass 2: one workgroup adds the partials into out */
-__global__ __launch_bounds__(kBlock) void ChecksumFinishKernel(const unsigned long long *partial,
-                                                              int nparts,
-                                                              unsigned long long *out) {
-  unsigned long long s1 = 0, s2 = 0;
-  for (int i = threadIdx.x; i < nparts; i += kBlock) {
-    s1 += partial[2 * i];
-    s2 += partial[2 * i + 1];
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire: every other workgroup's partial
+  s1 = s2 = 0;
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kBlock) {
+    s1 += __hip_atomic_load(&partial[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s2 += __hip_atomic_load(&partial[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   BlockSum2(s1, s2);
   if (threadIdx.x == 0) {
     out[0] += s1;
     out[1] += s2;
+    *arrived = 0;  // re-armed for the next launch on this device (stream order)
   }
 }
 
@@ -625,7 +530,9 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
   if (nbytes % 16 != 0 || !Aligned16(buf)) return hipErrorInvalidValue;
   const size_t nvec = nbytes / 16;
   if (nvec == 0) return hipSuccess;
-  // per-device partials scratch (2 x kChecksumGrid u64), allocated once per device
+  // per-device scratch: 2 x kChecksumGrid u64 partials + the arrival counter (zeroed once;
+  // the last workgroup of every launch re-arms it).  Launches of one device must not overlap
+  // (they are stream-ordered in the engine).
   static std::mutex mu;
   static std::map<int, unsigned long long *> scratch;
   int dev = 0;
@@ -637,7 +544,11 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
     auto it = scratch.find(dev);
     if (it == scratch.end()) {
       void *p = nullptr;
-      e = hipMalloc(&p, sizeof(unsigned long long) * 2 * kChecksumGrid);
+      const size_t bytes = sizeof(unsigned long long) * (2 * kChecksumGrid + 1);
+      e = hipMalloc(&p, bytes);
+      if (e != hipSuccess) return e;
+      e = hipMemset(p, 0, bytes);
+      if (e == hipSuccess) e = hipDeviceSynchronize();
       if (e != hipSuccess) return e;
       it = scratch.emplace(dev, static_cast<unsigned long long *>(p)).first;
     }
@@ -645,10 +556,9 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
   }
   constexpr int U = 4;
   const unsigned grid = std::min<unsigned>(TileGrid(nvec, U), kChecksumGrid);
-  hipLaunchKernelGGL(ChecksumPartialKernel<U>, dim3(grid), dim3(kBlock), 0, stream,
-                     static_cast<const uint4 *>(buf), nvec, partial);
-  hipLaunchKernelGGL(ChecksumFinishKernel, dim3(1), dim3(kBlock), 0, stream,
-                     static_cast<const unsigned long long *>(partial), static_cast<int>(grid), out);
+  hipLaunchKernelGGL(ChecksumKernel<U>, dim3(grid), dim3(kBlock), 0, stream,
+                     static_cast<const uint4 *>(buf), nvec, partial,
+                     reinterpret_cast<unsigned int *>(partial + 2 * kChecksumGrid), out);
   return hipGetLastError();
 }
 

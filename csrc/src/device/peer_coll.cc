@@ -61,13 +61,17 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
     : device_(device), stage_bytes_(RoundUp(std::max<size_t>(stage_bytes, 1 << 20), 1 << 16)),
       stream_(stream), heap_(heap) {
   CheckHip(hipSetDevice(device_), "hipSetDevice");
+  // fused allreduce: a segment is at most a stage, a tile kFusedTileBytes
+  tiles_cap_ = static_cast<int>((stage_bytes_ + kFusedTileMinBytes - 1) / kFusedTileMinBytes);
+  fused_block_bytes_ = RoundUp(FusedFlagWords(tiles_cap_) * sizeof(unsigned long long), 1 << 16);
+  const size_t flag_bytes = kPeerFlagBytes + 2 * fused_block_bytes_;
   void *p = nullptr;
   // uncached: peers poll the flags and stream the stage buffers over xGMI; nothing of it may
   // linger in a (non-coherent) L2 between ops
-  CheckHip(hipExtMallocWithFlags(&p, kPeerFlagBytes + 2 * stage_bytes_, hipDeviceMallocUncached),
+  CheckHip(hipExtMallocWithFlags(&p, flag_bytes + 2 * stage_bytes_, hipDeviceMallocUncached),
            "hipExtMallocWithFlags(peer stage)");
   base_ = static_cast<char *>(p);
-  CheckHip(hipMemset(base_, 0, kPeerFlagBytes), "hipMemset(flags)");
+  CheckHip(hipMemset(base_, 0, flag_bytes), "hipMemset(flags)");
   CheckHip(hipDeviceSynchronize(), "hipDeviceSynchronize");
   hipIpcMemHandle_t h;
   CheckHip(hipIpcGetMemHandle(&h, base_), "hipIpcGetMemHandle");
@@ -79,6 +83,7 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
   local_.pid = static_cast<int32_t>(getpid());
   local_.device = device_;
   local_.heap_bytes = heap_.base != nullptr ? heap_.bytes : 0;
+  local_.fused_cap = FusedResidentBlocks(device_);
   std::memcpy(local_.heap_ipc, heap_.ipc, sizeof(local_.heap_ipc));
   void *tbl = nullptr;
   CheckHip(hipMalloc(&tbl, kMaxPeers * sizeof(void *)), "hipMalloc(source table)");
@@ -166,12 +171,30 @@ bool PeerGroup::Open(const std::vector<PeerRecord> &all, int rank, std::string *
   }
   n_ = n;
   rank_ = rank;
+  // a fused launch waits on the other ranks' launches: when ranks share a GPU, no rank's grid
+  // may take every slot of it, or the others' workgroups could never start; each gets at most
+  // its share of the resident capacity.  Every rank derives the same grid from the same records
+  // (the launch's no-deadlock argument needs equal grids).
+  int share = 1;
+  for (int a = 0; a < n; ++a) {
+    int c = 0;
+    for (int b = 0; b < n; ++b) c += std::strncmp(all[a].pci, all[b].pci, sizeof(all[a].pci)) == 0;
+    share = std::max(share, c);
+  }
+  // capacity of an MI355X (256 CUs x 4 resident workgroups), lowered by what any rank's GPU
+  // reports, so that all ranks use the same value
+  int cap = 1024;
+  for (int a = 0; a < n; ++a) {
+    if (all[a].fused_cap > 0) cap = std::min(cap, static_cast<int>(all[a].fused_cap));
+  }
+  fused_grid_ = fused_grid_req_ > 0 ? fused_grid_req_ : std::max(16, cap / share);
   opened_ = true;
   return true;
 }
 
 char *PeerGroup::stage(int rank, int which) const {
-  return peer_base_[rank] + kPeerFlagBytes + static_cast<size_t>(which) * stage_bytes_;
+  return peer_base_[rank] + kPeerFlagBytes + 2 * fused_block_bytes_ +
+         static_cast<size_t>(which) * stage_bytes_;
 }
 
 void PeerGroup::SignalAbort() {
@@ -238,6 +261,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // per-phase timing of single-chunk ops (rabit_device_phase_timing=1)
   const bool timed = timing_ && count <= chunk;
   auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
+  bool did_fused = false;
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
     const int which = parity_;
@@ -259,6 +283,53 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     const bool zero_copy = indirect && !oneshot && !use_push && stage_prep == kPrepCopy &&
                            InHeap(chunk_src, c * tn) &&
                            (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
+    char *chunk_out = out + off * tn;
+    char *chunk_out2 = out2 != nullptr ? out2 + off * tn : nullptr;
+    // every input of this decision is the same on all ranks (the kernel copes with this rank's
+    // unaligned buffers itself), so all ranks run the same form of the chunk
+    if (fused_ && !oneshot && builtin_op >= 0 && c * tn >= fused_min_bytes_) {
+      // one launch for the whole chunk (per-tile hand-offs instead of two GPU-wide barriers)
+      FusedAllreduceArgs fa{};
+      for (int p = 0; p < n_; ++p) {
+        fa.stage[p] = stage(p, which);
+        fa.alloc[p] = peer_base_[p];
+        fa.heap[p] = peer_heap_.empty() ? nullptr : peer_heap_[p];
+        fa.flags[p] = fused_flags(p, which);
+      }
+      fa.src = chunk_src;
+      fa.out = chunk_out;
+      fa.out2 = chunk_out2;
+      fa.count = c;
+      fa.seg = seg;
+      // about one tile per workgroup of the grid, 8-64 KiB, a multiple of 256 elements
+      const size_t per_wg = RoundUp(seg * tn / static_cast<size_t>(fused_grid_), 256 * tn);
+      fa.tile = std::min(kFusedTileBytes, std::max(kFusedTileMinBytes, per_wg)) / tn;
+      fa.tiles = static_cast<int>((seg + fa.tile - 1) / fa.tile);
+      fa.tiles_cap = tiles_cap_;
+      fa.n = n_;
+      fa.rank = rank_;
+      fa.push = use_push ? 1 : 0;
+      fa.zero_copy = zero_copy ? 1 : 0;
+      fa.mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(chunk_src - heap_.base))
+                             : static_cast<unsigned long long>(mine - base_);
+      fa.epoch = ++fused_epoch_;
+      fa.dtype = dtype;
+      fa.op = builtin_op;
+      fa.prep = stage_prep;
+      fa.alpha = alpha;
+      fa.post = post_scale ? alpha : 0.0;
+      fa.abort_word = &host_words_[0];
+      fa.dev_status = dev_status();
+      fa.host_status = &host_words_[1];
+      fa.deadline_ticks = deadline_ticks_;
+      const int grid = std::min(fused_grid_, fa.tiles);
+      XRABIT_TRY_HIP(LaunchFusedAllreduce(fa, grid, stream_));
+      ++fused_chunks_;
+      did_fused = true;
+      if (use_push) ++push_chunks_;
+      if (zero_copy) ++zero_copy_chunks_;
+      continue;
+    }
     XRABIT_TRY_HIP(mark(0));
     if (use_push) {
       // no staging: this rank's own stage is its inbox, written by the peers
@@ -389,7 +460,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     XRABIT_TRY_HIP(mark(5));
   }
-  timing_pending_ = timed;
+  timing_pending_ = timed && !did_fused;  // phases exist only in the classic form
   return hipSuccess;
 }
 

@@ -87,6 +87,55 @@ struct ResolveArgs {
   const void **table;               // out: n source pointers
 };
 
+/*!
+ * \brief the fused two-shot allreduce of one chunk (fused_allreduce.hip): ONE launch replaces
+ *        stage copy + barrier + reduce + barrier + gather.  The chunk is cut into n segments
+ *        (segment q reduced by rank q) of `tiles` tiles each; workgroup w owns tiles
+ *        w, w + G, ... of every segment, on every rank, and hands them over with per-tile flags
+ *        instead of whole-GPU barriers:
+ *          1. stage (pull: own stage; push: inbox slot `rank` of each owner's stage) its tiles of
+ *             every segment, then raise ready[tile] (push: inbox[rank][tile] at each owner);
+ *          2. for its tiles of segment `rank`: wait for every rank's ready flag, reduce the n
+ *             sources in rank order into out/out2 and into the own stage (where peers gather
+ *             it), raise done[tile];
+ *          3. for its tiles of every other segment p: wait for done[tile] of rank p, copy.
+ *        A workgroup only ever waits for the workgroup with the SAME index on another rank, which
+ *        produces before it waits, so the launch cannot deadlock whatever subset of either grid
+ *        is resident (grids are equal on every rank).  Every wait gives up on the host abort
+ *        word, the wall-clock deadline, or a failure seen by another workgroup.
+ */
+constexpr size_t kFusedTileBytes = 64 * 1024;     // largest tile
+constexpr size_t kFusedTileMinBytes = 8 * 1024;   // smallest tile (small chunks, big grids)
+struct FusedAllreduceArgs {
+  char *stage[kMaxPeers];                 // stage buffer of this parity, per rank (mapped)
+  const char *alloc[kMaxPeers];           // exported allocation base per rank (zero copy)
+  const char *heap[kMaxPeers];            // symmetric heap base per rank (zero copy)
+  unsigned long long *flags[kMaxPeers];   // fused flag block of this parity, per rank
+  const char *src;                        // this rank's input chunk
+  char *out, *out2;                       // result chunk (out2: optional second copy)
+  size_t count;                           // elements in the chunk
+  size_t seg;                             // elements per segment (multiple of 256)
+  size_t tile;                            // elements per tile (multiple of 256)
+  int tiles;                              // tiles per segment
+  int tiles_cap;                          // flag slots per array in a flag block
+  int n, rank, push, zero_copy;
+  unsigned long long mailbox;             // zero copy: where this rank's input is
+  unsigned long long epoch;
+  int dtype, op, prep;
+  double alpha, post;
+  const volatile int *abort_word;
+  int *dev_status, *host_status;
+  long long deadline_ticks;
+};
+/*! \brief u64 words of one fused flag block (one parity) for tiles_cap tiles per segment */
+inline size_t FusedFlagWords(int tiles_cap) {
+  return 64 + static_cast<size_t>(2 + kMaxPeers) * static_cast<size_t>(tiles_cap);
+}
+/*! \brief workgroups of the fused kernel that fit on `device` at once (0: unknown) */
+int FusedResidentBlocks(int device);
+/*! \brief enqueue the fused allreduce of one chunk on `grid` workgroups */
+hipError_t LaunchFusedAllreduce(const FusedAllreduceArgs &args, int grid, hipStream_t stream);
+
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
                              const volatile int *abort_word, int *dev_status, int *host_status,
                              long long deadline_ticks, const ResolveArgs *resolve,
@@ -103,6 +152,8 @@ struct PeerRecord {
   int32_t device;
   char heap_ipc[64];   // hipIpcMemHandle_t of the symmetric heap (heap_bytes != 0)
   uint64_t heap_bytes;
+  int32_t fused_cap;   // fused-kernel workgroups resident at once on this GPU
+  int32_t pad;
 };
 
 /*!
@@ -188,6 +239,18 @@ class PeerGroup {
   bool push() const { return push_; }
   uint64_t push_chunks() const { return push_chunks_; }
   uint64_t oneshot_ops() const { return oneshot_ops_; }
+  /*!
+   * \brief two-shot chunks of built-in ops run as ONE fused kernel (per-tile flags, see
+   *        FusedAllreduceArgs) instead of stage + barrier + reduce + barrier + gather launches
+   */
+  void set_fused(bool v) { fused_ = v; }
+  bool fused() const { return fused_; }
+  /*! \brief workgroups of a fused launch (0: automatic, from the ranks sharing a GPU) */
+  void set_fused_grid(int g) { fused_grid_req_ = g; }
+  /*! \brief chunks below this many bytes keep the classic form */
+  void set_fused_min_bytes(size_t b) { fused_min_bytes_ = b; }
+  int fused_grid() const { return fused_grid_; }
+  uint64_t fused_chunks() const { return fused_chunks_; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
   /*! \brief fold the last timed op into the phase totals (call after the stream drained) */
@@ -210,6 +273,11 @@ class PeerGroup {
     return heap_.base != nullptr && c >= heap_.base && c + bytes <= heap_.base + heap_.bytes;
   }
   char *stage(int rank, int which) const;
+  /*! \brief fused flag block of `rank` for stage parity `which` */
+  unsigned long long *fused_flags(int rank, int which) const {
+    return reinterpret_cast<unsigned long long *>(peer_base_[rank] + kPeerFlagBytes +
+                                                  static_cast<size_t>(which) * fused_block_bytes_);
+  }
   int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
   void NewBatch(CopyBatch *b) const {
     b->n = 0;
@@ -241,6 +309,13 @@ class PeerGroup {
   uint64_t oneshot_ops_{0};
   bool push_{false};
   uint64_t push_chunks_{0};
+  bool fused_{true};
+  int fused_grid_req_{0}, fused_grid_{256};
+  size_t fused_min_bytes_{0};
+  int tiles_cap_{0};                // flag slots per array of a fused flag block
+  size_t fused_block_bytes_{0};     // bytes of one fused flag block (2 per allocation)
+  unsigned long long fused_epoch_{0};
+  uint64_t fused_chunks_{0};
 };
 
 }  // namespace device

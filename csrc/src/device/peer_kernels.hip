@@ -14,8 +14,8 @@
  *
  * Copy batch: up to kMaxCopySegs (dst, src[, dst2]) segments in one launch; workgroup b takes
  * tile b / nseg of segment b % nseg, so the workgroups in flight read from every peer at once
- * and all xGMI links carry traffic together.  Tiles are 256 lanes x 4 x 16 B like the other
- * streaming kernels (kernels.hip).
+ * and all xGMI links carry traffic together.  Tiles are 256 lanes x 16 B (kUnroll = 1: 4 KiB per
+ * workgroup), like the other streaming kernels (kernels.hip).
  */
 #include <hip/hip_runtime.h>
 

@@ -72,6 +72,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_mock_dev_hang_sec")) dev_hang_max_sec_ = atof(val);
   if (is("rabit_device_spin_us")) dcfg_.spin_us = atoi(val);
   if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
+  if (is("rabit_device_spill_cap")) dcfg_.spill_cap = core::ParseUnit(name, val);
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
   if (is("rabit_device_algo")) {
     const std::string v(val);
@@ -97,6 +98,12 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
   if (is("rabit_device_oneshot_max")) dcfg_.oneshot_max = core::ParseUnit(name, val);
+  if (is("rabit_device_fused")) {
+    // auto: the calibration picks (without a calibration: the classic form)
+    dcfg_.fused_mode = !strcmp(val, "auto") ? 2 : (utils::StringToBool(val) ? 1 : 0);
+  }
+  if (is("rabit_device_fused_grid")) dcfg_.fused_grid = atoi(val);
+  if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
     if (!strcmp(val, "auto")) {
       dcfg_.direct_mode = 0;
@@ -454,35 +461,56 @@ Status EngineBase::CalibrateDevice() {
     for (size_t i = 0; i < sizes[k] && ok; ++i) ok = host[i] == want ? 1 : 0;
     if (!ok) utils::HandleLogInfo("[%d] direct transport verification failed\n", rank_);
   }
-  // 1b. the push variant of the direct reduce-scatter (remote writes) at the large size;
-  //     verified like the pull one.  A failed run disables the direct transport altogether (a
-  //     failed barrier drops the group); a wrong result only rules push out.
-  int push_ok = ok && dcfg_.direct_mode == 0 ? 1 : 0;
-  double t_push = 0;
-  if (push_ok) {
-    const double t_pull = t[1][1];
-    dev_->SetDirectPush(true);
+  // 1b. the other forms of the direct two-shot path at the large size, each verified like the
+  //     first: push (remote writes) instead of pull, and the fused single-kernel form instead
+  //     of the 5-launch one (or the reverse).  A failed run disables the direct transport
+  //     altogether (a failed barrier drops the group); a wrong result only rules that form out.
+  //     Variant 0 is the form step 1 measured.
+  const bool fused_auto = dcfg_.fused_mode == 2;
+  const bool cfg_fused = dcfg_.fused_mode == 1;  // auto starts from the classic form
+  struct Form {
+    bool push, fused;
+  };
+  Form forms[kCalibForms] = {{dcfg_.direct_mode == 2, cfg_fused},
+                             {dcfg_.direct_mode == 2, !cfg_fused},
+                             {true, cfg_fused},
+                             {true, !cfg_fused}};
+  int form_ok[kCalibForms] = {ok, 0, 0, 0};
+  double t_form[kCalibForms] = {t[1][1], 0, 0, 0};
+  const bool try_push = dcfg_.direct_mode == 0;
+  for (int f = 1; f < kCalibForms && ok; ++f) {
+    if ((f == 1 || f == 3) && !fused_auto) continue;
+    if (f >= 2 && !try_push) continue;
+    dev_->SetDirectPush(forms[f].push);
+    dev_->SetFused(forms[f].fused);
     Status st;
     if (!measure(1, 1, &st)) {
       ok = 0;
-      push_ok = 0;
-    } else {
-      t_push = t[1][1];
-      host.resize(sizes[1]);
-      dev_->StageToHost(host.data(), dst, sizes[1] * 4);
-      for (size_t i = 0; i < sizes[1] && push_ok; ++i) push_ok = host[i] == want ? 1 : 0;
-      if (!push_ok) utils::HandleLogInfo("[%d] direct push verification failed\n", rank_);
+      break;
     }
-    t[1][1] = t_pull;
-    if (dev_->has_peers()) dev_->SetDirectPush(false);
+    t_form[f] = t[1][1];
+    host.resize(sizes[1]);
+    dev_->StageToHost(host.data(), dst, sizes[1] * 4);
+    form_ok[f] = 1;
+    for (size_t i = 0; i < sizes[1] && form_ok[f]; ++i) form_ok[f] = host[i] == want ? 1 : 0;
+    if (!form_ok[f]) {
+      utils::HandleLogInfo("[%d] direct %s %s verification failed\n", rank_,
+                           forms[f].push ? "push" : "pull", forms[f].fused ? "fused" : "classic");
+    }
+  }
+  t[1][1] = t_form[0];
+  if (dev_->has_peers()) {
+    dev_->SetDirectPush(forms[0].push);
+    dev_->SetFused(forms[0].fused);
   }
   dev_->ForceTransport(-1);
   dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
-  int flags[2] = {ok, push_ok};
-  Status s = host_->Allreduce(flags, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+  int flags[1 + kCalibForms] = {ok, form_ok[0], form_ok[1], form_ok[2], form_ok[3]};
+  Status s = host_->Allreduce(flags, sizeof(int), 1 + kCalibForms,
+                              coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
   ok = flags[0];
-  push_ok = flags[1];
+  for (int f = 0; f < kCalibForms; ++f) form_ok[f] = ok && flags[1 + f];
   // 2. RCCL (only worth timing when the direct transport is usable: the choice is uniform)
   if (ok) {
     for (int k = 0; k < 2; ++k) {
@@ -495,17 +523,24 @@ Status EngineBase::CalibrateDevice() {
     dev_->ForceTransport(-1);
   }
   // identical decision everywhere: max time over ranks
-  double agg[5] = {t[0][0], t[0][1], t[1][0], t[1][1], t_push};
-  s = host_->Allreduce(agg, sizeof(double), 5, coll::HostReducer(mpi::kDouble, mpi::kMax));
+  double agg[4 + kCalibForms] = {t[0][0], t[0][1], t[1][0], t[1][1],
+                                 t_form[0], t_form[1], t_form[2], t_form[3]};
+  s = host_->Allreduce(agg, sizeof(double), 4 + kCalibForms,
+                       coll::HostReducer(mpi::kDouble, mpi::kMax));
   if (s != Status::kSuccess) return s;
   size_t threshold = static_cast<size_t>(-1);
+  int best = 0;
   if (!ok) {
     dev_->DropPeers();
   } else {
-    // pull or push for the two-shot path: the faster one at the large size (same everywhere)
-    const bool use_push = push_ok && agg[4] < agg[3];
-    dev_->SetDirectPush(use_push);
-    if (use_push) agg[3] = agg[4];
+    // the form of the two-shot path: the fastest verified one at the large size (same
+    // everywhere: times and verdicts were agreed on above)
+    for (int f = 1; f < kCalibForms; ++f) {
+      if (form_ok[f] && agg[4 + f] < agg[4 + best]) best = f;
+    }
+    dev_->SetDirectPush(forms[best].push);
+    dev_->SetFused(forms[best].fused);
+    agg[3] = agg[4 + best];
     // linear model t = a + b * bytes per transport through the two points; direct from the
     // crossover on (when its slope is smaller)
     const double x0 = sizes[0] * 4.0, x1 = sizes[1] * 4.0;
@@ -518,14 +553,16 @@ Status EngineBase::CalibrateDevice() {
     dev_->set_direct_min_bytes(threshold);
   }
   calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
-            static_cast<double>(sizes[1] * 4), agg[4]};
+            static_cast<double>(sizes[1] * 4), agg[4 + 2] > 0 ? agg[4 + 2] : 0.0};
+  for (int f = 0; f < kCalibForms; ++f) calib_form_us_[f] = form_ok[f] ? agg[4 + f] * 1e6 : -1.0;
   calib_heap_src_ = heap_src;
   if (debug_ || rank_ == 0) {
     utils::HandleLogInfo(
         "[xrabit] device calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B rccl "
-        "%.1f us direct %.1f us (push %.1f us, %s) -> direct %s\n",
+        "%.1f us direct %.1f us (%s %s; forms %.1f %.1f %.1f %.1f us) -> direct %s\n",
         n, sizes[0] * 4, agg[0] * 1e6, agg[2] * 1e6, sizes[1] * 4, agg[1] * 1e6, agg[3] * 1e6,
-        agg[4] * 1e6, dev_->direct_push() ? "push" : "pull",
+        dev_->direct_push() ? "push" : "pull", forms[best].fused ? "fused" : "classic",
+        calib_form_us_[0], calib_form_us_[1], calib_form_us_[2], calib_form_us_[3],
         !ok ? "disabled (failed verification)"
             : (threshold == static_cast<size_t>(-1) ? "off (RCCL faster)"
                                                     : ("from " + std::to_string(threshold) + " B").c_str()));
@@ -879,12 +916,17 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
      << ",\"oneshot_ops\":" << (dev_ ? dev_->oneshot_ops() : 0)
+     << ",\"fused_chunks\":" << (dev_ ? dev_->fused_chunks() : 0)
+     << ",\"fused_grid\":" << (dev_ ? dev_->fused_grid() : 0)
      << ",\"symmetric_heap_used\":" << (dev_ ? dev_->sym_heap_used() : 0)
      << ",\"device_direct_min\":"
      << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
      << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
      << ",\"calib_push_us\":" << calib_.push_big * 1e6
+     << ",\"calib_forms_us\":[" << calib_form_us_[0] << "," << calib_form_us_[1] << ","
+     << calib_form_us_[2] << "," << calib_form_us_[3] << "]"
+     << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)
@@ -913,7 +955,12 @@ std::string EngineBase::StatsJson() const {
      << ",\"t_broadcast\":" << s.t_broadcast << ",\"t_allgather\":" << s.t_allgather
      << ",\"t_checkpoint\":" << s.t_checkpoint << ",\"t_consensus\":" << s.t_consensus
      << ",\"t_recover\":" << s.t_recover
-     << ",\"device_log_bytes\":" << (dev_ ? dev_->arena()->used() : 0) << "}";
+     << ",\"n_spilled_results\":" << s.n_spilled_results
+     << ",\"n_spilled_replays\":" << s.n_spilled_replays
+     << ",\"bytes_spilled\":" << s.bytes_spilled
+     << ",\"device_log_bytes\":" << (dev_ ? dev_->arena()->used() : 0)
+     << ",\"device_spill_bytes\":"
+     << (dev_ && dev_->spill_arena() ? dev_->spill_arena()->used() : 0) << "}";
   return os.str();
 }
 }  // namespace engine

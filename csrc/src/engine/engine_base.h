@@ -37,6 +37,9 @@ struct EngineStats {
   uint64_t n_consensus_elided{0};
   uint64_t n_device_replays{0};
   uint64_t n_device_ckpt_loads{0};  // checkpoint loads served over the device plane
+  uint64_t n_spilled_results{0};    // HBM results logged in pinned host memory (log cap hit)
+  uint64_t n_spilled_replays{0};    // replays served from a spilled result
+  double bytes_spilled{0};
   double bytes_local_in{0};   // local-checkpoint replica bytes received over the device plane
   double bytes_replay_in{0};  // recovered result bytes received over the device plane
   double bytes_ckpt_in{0};    // global-checkpoint bytes received over the device plane
@@ -236,6 +239,10 @@ class EngineBase : public IEngine {
   struct {
     double rccl_small, rccl_big, direct_small, direct_big, small_bytes, big_bytes, push_big;
   } calib_{0, 0, 0, 0, 0, 0, 0};
+  /*! \brief forms of the direct two-shot path the calibration times at its large size:
+   *  {configured, other fused/classic, push configured-fused, push other}; us, -1 = not run */
+  static constexpr int kCalibForms = 4;
+  double calib_form_us_[kCalibForms]{-1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
   bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
   double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long

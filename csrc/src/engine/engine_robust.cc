@@ -42,14 +42,20 @@ void *EngineRobust::ResultLog::HostArena::Alloc(size_t bytes) {
     ++cur_;
   }
   Chunk c;
-  // 2 MiB aligned and backed by transparent huge pages where the kernel allows it: a result
-  // log chunk is written once per op in full, and 4 KiB first-touch faults on fresh chunks
-  // cost as much as the copy itself
+  // big chunks are 2 MiB aligned and backed by transparent huge pages where the kernel allows
+  // it: a result log chunk is written once per op in full, and 4 KiB first-touch faults on
+  // fresh chunks cost as much as the copy itself.  Logs of short keys use small chunks.
   constexpr size_t kHuge = 2u << 20;
-  c.size = (std::max<size_t>(need, 64u << 20) + kHuge - 1) & ~(kHuge - 1);
-  c.base = static_cast<char *>(std::aligned_alloc(kHuge, c.size));
+  const size_t want = std::max(need, min_chunk_);
+  if (want >= kHuge) {
+    c.size = (want + kHuge - 1) & ~(kHuge - 1);
+    c.base = static_cast<char *>(std::aligned_alloc(kHuge, c.size));
+    if (c.base != nullptr) (void)madvise(c.base, c.size, MADV_HUGEPAGE);
+  } else {
+    c.size = (want + 63) & ~static_cast<size_t>(63);
+    c.base = static_cast<char *>(std::aligned_alloc(64, c.size));
+  }
   utils::Check(c.base != nullptr, "out of host memory for the result log (%zu bytes)", c.size);
-  (void)madvise(c.base, c.size, MADV_HUGEPAGE);
   c.used = need;
   chunks_.push_back(c);
   cur_ = chunks_.size() - 1;
@@ -78,18 +84,30 @@ void EngineRobust::ResultLog::Clear() {
   entries_.clear();
   host_.Reset();
   if (arena_ != nullptr) arena_->Reset();
+  if (spill_ != nullptr) spill_->Reset();
 }
 
 void *EngineRobust::ResultLog::AllocTemp(size_t size, bool device) {
   utils::Assert(size != 0, "cannot log a zero-size result");
-  temp_ = Entry{-1, size, device, nullptr};
+  temp_ = Entry{-1, size, device, nullptr, false};
   if (device) {
     utils::Check(arena_ != nullptr, "device result without a device arena");
     void *p = arena_->Alloc(size);
+    if (p == nullptr && spill_ != nullptr) {
+      // the HBM log reached rabit_device_log_cap (or HBM is full): keep this result in pinned
+      // host memory, like the reference's unbounded host log (allreduce_robust.h:324-388)
+      p = spill_->Alloc(size);
+      if (p != nullptr) {
+        temp_.on_device = false;
+        temp_.spilled = true;
+        n_spilled_ += 1;
+      }
+    }
     utils::Check(p != nullptr,
-                 "device result log is full (%zu bytes logged since the last checkpoint); "
-                 "checkpoint more often or raise rabit_device_log_cap",
-                 arena_->used());
+                 "device result log is full (%zu bytes in HBM since the last checkpoint, %zu "
+                 "spilled to host); checkpoint more often or raise rabit_device_log_cap / "
+                 "rabit_device_spill_cap",
+                 arena_->used(), spill_ != nullptr ? spill_->used() : size_t(0));
     temp_.ptr = p;
     return p;
   }
@@ -117,7 +135,9 @@ void EngineRobust::ResultLog::DropLast() {
   utils::Assert(!entries_.empty(), "nothing to drop");
   const Entry e = entries_.back();
   entries_.pop_back();
-  if (e.on_device) {
+  if (e.spilled) {
+    if (spill_ != nullptr) spill_->PopTo(e.ptr);
+  } else if (e.on_device) {
     if (arena_ != nullptr) arena_->PopTo(e.ptr);
   } else {
     host_.PopTo(e.ptr);
@@ -164,7 +184,10 @@ bool EngineRobust::Init(int argc, char *argv[]) {
   checkpoint_loaded_ = false;
   result_buffer_round_ =
       num_global_replica_ == 0 ? -1 : std::max(GetWorldSize() / num_global_replica_, 1);
-  if (dev_) resbuf_.SetArena(dev_->arena());
+  if (dev_) resbuf_.SetArena(dev_->arena(), dev_->spill_arena());
+  // the bootstrap cache logs keys (short strings) and small early results
+  lookupbuf_.SetHostChunk(64u << 10);
+  cachebuf_.SetHostChunk(1u << 20);
   if (timeout_enabled_ || hang_timeout_sec_ > 0 || (dev_ && dev_wait_limit_sec_ > 0)) {
     StartWatchdog();
   }
@@ -223,6 +246,16 @@ void EngineRobust::CopyAny(void *dst, bool dst_dev, const void *src, bool src_de
   dev_->EnterFromUser();
   dev_->CopyAsync(dst, src, n);
   utils::Check(dev_->Finish(MakeProbe(), true) == Status::kSuccess, "device copy failed");
+}
+
+void EngineRobust::SpillResult(void *slot, const void *src, size_t n) {
+  // stream-ordered D2H: later work on the caller's stream (which may overwrite src) runs after
+  // it; a reader of the slot on the host synchronises first (TryGetResult)
+  dev_->EnterFromUser();
+  dev_->CopyAsync(slot, src, n);
+  dev_->Finish(MakeProbe(), false);
+  stats_.n_spilled_results += 1;
+  stats_.bytes_spilled += static_cast<double>(n);
 }
 
 // ------------------------------------------------------------------ collectives
@@ -312,9 +345,10 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
   ApplyRetention();
   if (!recovered) run_prepare();
   void *temp = resbuf_.AllocTemp(bytes, dev);
+  const bool spilled = resbuf_.temp_spilled();
   for (;;) {
     if (recovered) {
-      CopyAny(temp, dev, buf, dev, bytes);
+      CopyAny(temp, dev && !spilled, buf, dev, bytes);
       stats_.n_recovered_ops += 1;
       break;
     }
@@ -322,9 +356,12 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
     if (dev) {
       // the collective writes the log slot, and the user buffer only once it succeeded on this
       // rank, so a retry still finds the input (prep_src: the prepare pass runs in the
-      // transport and is skipped entirely when the result is recovered)
-      s = TryAllreduceDevice(prep_src != nullptr ? prep_src : buf, temp, spec, buf,
+      // transport and is skipped entirely when the result is recovered).  A spilled slot is
+      // host memory: the collective writes an HBM stage, copied to the slot behind it.
+      void *slot = spilled ? dev_->Scratch(bytes, device::DevicePlane::kSpillScratch) : temp;
+      s = TryAllreduceDevice(prep_src != nullptr ? prep_src : buf, slot, spec, buf,
                              prep_src != nullptr ? prep_op : device::kPrepCopy, prep_alpha);
+      if (s == Status::kSuccess && spilled) SpillResult(temp, slot, bytes);
     } else {
       // out of place: the log slot receives the result, buf keeps the input until success
       if (host_out_of_place_) {
@@ -377,12 +414,14 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
   void *temp = resbuf_.AllocTemp(total_size, dev);
   for (;;) {
     if (recovered) {
-      CopyAny(temp, dev, buf, dev, total_size);
+      CopyAny(temp, dev && !resbuf_.temp_spilled(), buf, dev, total_size);
       stats_.n_recovered_ops += 1;
       break;
     }
     if (CheckAndRecover(TryBroadcast(buf, total_size, root))) {
-      if (dev) {
+      if (dev && resbuf_.temp_spilled()) {
+        SpillResult(temp, buf, total_size);
+      } else if (dev) {
         dev_->CopyDeviceAsync(temp, buf, total_size);
         dev_->Finish(MakeProbe(), false);
       } else {
@@ -431,14 +470,16 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
   void *temp = resbuf_.AllocTemp(total_size, dev);
   for (;;) {
     if (recovered) {
-      CopyAny(temp, dev, buf, dev, total_size);
+      CopyAny(temp, dev && !resbuf_.temp_spilled(), buf, dev, total_size);
       stats_.n_recovered_ops += 1;
       break;
     }
     // in place on the user buffer: the ring never overwrites this rank's own slice, so a
     // retry after a failure still finds its input
     if (CheckAndRecover(TryAllgather(buf, total_size, slice_begin, slice_end, size_prev_slice))) {
-      if (dev) {
+      if (dev && resbuf_.temp_spilled()) {
+        SpillResult(temp, buf, total_size);
+      } else if (dev) {
         dev_->CopyDeviceAsync(temp, buf, total_size);
         dev_->Finish(MakeProbe(), false);
       } else {

@@ -127,13 +127,25 @@ class EngineRobust : public EngineBase {
     struct Entry {
       int seqno;
       size_t size;
-      bool on_device;
-      void *ptr;  // host arena or HBM arena slot
+      bool on_device;  // ptr is HBM
+      void *ptr;       // host arena, HBM arena or pinned spill slot
+      bool spilled;    // result of an HBM op kept in pinned host memory (HBM log was full)
     };
-    void SetArena(device::DeviceArena *a) { arena_ = a; }
+    /*! \brief HBM arena for device results, and the pinned arena they spill to past its cap */
+    void SetArena(device::DeviceArena *a, device::DeviceArena *spill) {
+      arena_ = a;
+      spill_ = spill;
+    }
+    /*! \brief growth step of the host arena (small for logs of short keys) */
+    void SetHostChunk(size_t bytes) { host_.set_min_chunk(bytes); }
     void Clear();
-    /*! \brief scratch slot for the next result (not visible until PushTemp) */
+    /*!
+     * \brief scratch slot for the next result (not visible until PushTemp).  A device result
+     *        that does not fit the HBM arena spills to pinned host memory (temp_spilled()).
+     */
     void *AllocTemp(size_t size, bool device);
+    bool temp_spilled() const { return temp_.spilled; }
+    size_t n_spilled() const { return n_spilled_; }
     void PushTemp(int seqno, size_t size);
     /*! \brief stored entry for seqno or nullptr */
     const Entry *Query(int seqno) const;
@@ -152,6 +164,7 @@ class EngineRobust : public EngineBase {
       void *Alloc(size_t bytes);
       void PopTo(void *ptr);
       void Reset();
+      void set_min_chunk(size_t b) { min_chunk_ = b; }
 
      private:
       struct Chunk {
@@ -160,11 +173,14 @@ class EngineRobust : public EngineBase {
       };
       std::vector<Chunk> chunks_;
       size_t cur_{0};
+      size_t min_chunk_{64u << 20};
     };
     std::vector<Entry> entries_;
     HostArena host_;
     Entry temp_{};
     device::DeviceArena *arena_{nullptr};
+    device::DeviceArena *spill_{nullptr};
+    size_t n_spilled_{0};
   };
 
   // ---- collectives
@@ -175,6 +191,8 @@ class EngineRobust : public EngineBase {
                       bool lazy);
   /*! \brief drop the previous result unless this rank is one of its replicas */
   void ApplyRetention();
+  /*! \brief copy an HBM result into its pinned spill slot (stream-ordered) */
+  void SpillResult(void *slot, const void *src, size_t n);
   /*! \brief copy n bytes between host/device locations (synchronous w.r.t. the result) */
   void CopyAny(void *dst, bool dst_dev, const void *src, bool src_dev, size_t n);
 

@@ -311,6 +311,20 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
       size = e->size;
       data = resbuf_.Data(*e);
       data_dev = e->on_device;
+      if (e->spilled) {
+        stats_.n_spilled_replays += 1;
+        if (device_replay_) {
+          // served over xGMI like an HBM entry: back into the HBM stage first
+          void *stage = dev_->Scratch(size, device::DevicePlane::kSpillScratch);
+          dev_->EnterFromUser();
+          dev_->CopyAsync(stage, data, size);
+          data = stage;
+          data_dev = true;
+        } else {
+          // the TCP route reads the slot on the host: its D2H copy must have landed
+          dev_->Synchronize();
+        }
+      }
     } else {
       role = kPassData;
     }

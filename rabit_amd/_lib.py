@@ -85,6 +85,7 @@ def _declare(d: ctypes.CDLL) -> None:
                                              ctypes.POINTER(c_ulong), c_int,
                                              ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
         "RabitDevSetTransport": (c_int, [c_int, c_int]),
+        "RabitDevSetFused": (c_int, [c_int]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),
         "RabitTraceDump": (c_int, [c_char_p]),

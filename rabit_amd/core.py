@@ -403,14 +403,21 @@ TRANSPORT_RCCL = 0
 TRANSPORT_DIRECT = 1
 
 
-def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str] = None) -> bool:
+def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str] = None,
+                         fused: Optional[bool] = None) -> bool:
     """Route this rank's device collectives over one transport (benchmarks / diagnosis):
-    TRANSPORT_AUTO (the calibrated choice), TRANSPORT_RCCL or TRANSPORT_DIRECT, and pick the
-    direct reduce-scatter variant ("pull" / "push").  Every rank must make the same call between
-    the same collectives.  False when that transport is not up on this rank."""
+    TRANSPORT_AUTO (the calibrated choice), TRANSPORT_RCCL or TRANSPORT_DIRECT, pick the
+    direct reduce-scatter variant ("pull" / "push") and the form of the direct two-shot path
+    (fused=True: one kernel per chunk with per-tile hand-offs; False: the 5-launch form).
+    Every rank must make the same call between the same collectives.  False when that
+    transport is not up on this rank."""
     _check_init()
     mode = {None: 0, "pull": 1, "push": 2}[direct_mode]
-    return _LIB.RabitDevSetTransport(int(which), mode) == 0
+    if _LIB.RabitDevSetTransport(int(which), mode) != 0:
+        return False
+    if fused is not None:
+        return _LIB.RabitDevSetFused(1 if fused else 0) == 0
+    return True
 
 
 def last_error() -> str:

@@ -74,11 +74,13 @@ def prepare(dst, src, prep: int, alpha: float = 1.0, dst2=None):
     return dst
 
 
-def checksum(buf):
-    """(sum of 32-bit words, sum of (i+1)*word) mod 2^64 over the tensor's bytes."""
+def checksum(buf, out=None):
+    """(sum of 32-bit words, sum of (i+1)*word) mod 2^64 over the tensor's bytes, as a 2-element
+    int64 tensor; with `out` (zeroed int64[2] on the device) the sums are ADDED to it."""
     import torch
 
-    out = torch.zeros(2, dtype=torch.int64, device=buf.device)
+    if out is None:
+        out = torch.zeros(2, dtype=torch.int64, device=buf.device)
     _check(_dll().RabitDevChecksum(ctypes.c_void_p(buf.data_ptr()),
                                    buf.numel() * buf.element_size(),
                                    ctypes.c_void_p(out.data_ptr()), _stream(buf)),

@@ -26,6 +26,12 @@ assert lo == hi, (lo, hi)
 assert st["calib_push_us"] > 0, st
 push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
 assert push in (0, world), push
+# all four forms of the two-shot path (pull/push x classic/fused) were timed and verified, and
+# the chosen form is the same everywhere
+forms = st["calib_forms_us"]
+assert len(forms) == 4 and all(f > 0 for f in forms), forms
+fused = rabit.allreduce(np.array([st["direct_fused"]]), rabit.SUM)[0]
+assert fused in (0, world), fused
 # with a symmetric heap that has room, the calibration reads its inputs from the heap's tail
 want_heap = any(a.startswith("rabit_device_symmetric_heap=") for a in sys.argv[1:])
 assert st["calib_heap_src"] == (1 if want_heap else 0), st

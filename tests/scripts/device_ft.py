@@ -39,5 +39,6 @@ assert torch.all(w == expect), (float(w[0]), expect)
 st = rabit.stats()
 assert st["device_direct"] == 1, st
 rabit.finalize()
-print("[%d] DEVFT OK replays=%d recovered=%d" % (rank, st["n_device_replays"], st["n_recovered_ops"]),
-      flush=True)
+print("[%d] DEVFT OK replays=%d recovered=%d spilled=%d spilled_replays=%d"
+      % (rank, st["n_device_replays"], st["n_recovered_ops"], st["n_spilled_results"],
+         st["n_spilled_replays"]), flush=True)

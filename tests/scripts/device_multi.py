@@ -65,6 +65,21 @@ for dt in (np.int8, np.uint8, np.int32, np.int64, np.float32, np.float64):
             assert np.array_equal(got, exp), (dt, op, n, got[:8], exp[:8])
             checked += 1
 
+# a buffer at an odd element offset on odd ranks only (a view): the transport's choices stay the
+# same on every rank, only how this rank touches its own memory changes
+for dt in (np.float32, np.int8, np.float64):
+    for op in (rabit.SUM, rabit.MAX):
+        n = (3 << 20) // np.dtype(dt).itemsize + 5
+        vals = torch.from_numpy(values(rank, n, dt, op)).to(dev)
+        if rank % 2 == 1:
+            t = torch.empty(n + 1, dtype=vals.dtype, device=dev)[1:]
+            t.copy_(vals)
+        else:
+            t = vals
+        rabit.allreduce(t, op)
+        assert np.array_equal(t.cpu().numpy(), expected(n, dt, op)), ("unaligned", dt, op)
+        checked += 1
+
 # fused lazy-prepare: dst = sum over ranks of src^2
 n = (1 << 19) + 11
 src = torch.arange(n, device=dev, dtype=torch.float32).remainder_(17).add_(rank)

@@ -21,11 +21,13 @@ def _run(script, nworker, args=(), attempts=1, timeout=300, env=None):
     return rc, "".join("".join(o) for o in job.outputs)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_direct_collectives(world):
+def test_direct_collectives(world, fused):
+    """fused=1: two-shot chunks as one kernel with per-tile hand-offs; 0: the 5-launch form"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("device_multi.py", world)
+    rc, out = _run("device_multi.py", world, ["rabit_device_fused=" + fused])
     assert rc == 0, out[-5000:]
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
@@ -55,6 +57,23 @@ def test_direct_recovery(mock, mode):
         import re
         replays = [int(x) for x in re.findall(r"DEVFT OK replays=(\d+)", out)]
         assert sum(replays) > 0, out[-3000:]
+
+
+def test_result_log_spills_to_host():
+    """an HBM result log capped below one iteration's results: the entries past the cap live in
+    pinned host memory, and killed ranks replay both kinds (HBM and spilled) from survivors"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import re
+    rc, out = _run("device_ft.py", 3, ["mock=0,2,1,0", "mock=2,1,2,0", "rabit_device_log_cap=3M",
+                                       "rabit_device_log_chunk=2M"], attempts=4)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVFT OK") == 3, out[-3000:]
+    spilled = [int(x) for x in re.findall(r"DEVFT OK .* spilled=(\d+)", out)]
+    spill_replays = [int(x) for x in re.findall(r"spilled_replays=(\d+)", out)]
+    replays = [int(x) for x in re.findall(r"DEVFT OK replays=(\d+)", out)]
+    assert min(spilled) > 0, out[-3000:]
+    assert sum(spill_replays) > 0 and sum(replays) > 0, out[-3000:]
 
 
 def test_host_buffers_via_device():
@@ -121,8 +140,8 @@ def test_bench_torchrun_shared_gpu(n):
     # every available transport x input variant ran and matched the host fp64 reference
     ran = [v for v in rec["variants"] if v["available"]]
     assert {(v["transport"], v["input"]) for v in ran} >= {
-        ("direct-pull", "torch"), ("direct-push", "torch"), ("direct-pull", "symmetric"),
-        ("direct-push", "symmetric")}, rec["variants"]
+        ("direct-%s-%s" % (m, f), i) for m in ("pull", "push") for f in ("classic", "fused")
+        for i in ("torch", "symmetric")}, rec["variants"]
     assert all(v["check"] and v["t_us"] > 0 for v in ran), rec["variants"]
 
 

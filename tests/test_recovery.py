@@ -65,6 +65,20 @@ def test_python_local_recover(native_build):
     assert sum(a - 1 for a in job.attempts) >= 3
 
 
+@pytest.mark.parametrize("elide", ["1", "0"])
+def test_leaf_dies_during_small_broadcasts(native_build, elide):
+    """Leaves die inside runs of small broadcasts while each result is kept on only half of the
+    ranks (retention round 2): with consensus elision survivors may run ahead of the failure
+    before a link error stops them, and every rank must still end with the exact results."""
+    script = os.path.join(ROOT, "tests", "scripts", "bcast_leaf_fail.py")
+    rc, job, out = _run([sys.executable, script, "rabit_global_replica=5",
+                         "rabit_elide_consensus=" + elide, "mock=9,1,21,0", "mock=8,2,5,0",
+                         "mock=9,2,40,1", "mock=7,3,2,0"], timeout=300)
+    assert rc == 0, out[-4000:]
+    assert out.count("BCAST-LEAF OK") == 10, out[-3000:]
+    assert sum(a - 1 for a in job.attempts) >= 4
+
+
 def test_lazy_prepare_not_rerun_on_replay(native_build):
     """A restarted worker must not call prepare_fun for results it replays."""
     script = os.path.join(ROOT, "tests", "scripts", "lazy_prepare.py")

@@ -22,12 +22,14 @@ import rabit_amd as rabit
 
 def main():
     sym = os.environ.get("XR_SYM", "0") == "1"
-    rabit.init(sys.argv[1:], lib="base", rabit_device=0, rabit_device_phase_timing=1,
-               rabit_device_algo="direct",
+    fused = os.environ.get("XR_FUSED", "1")
+    timing = os.environ.get("XR_PHASE", "0")
+    rabit.init(sys.argv[1:], lib="base", rabit_device=0, rabit_device_phase_timing=timing,
+               rabit_device_algo="direct", rabit_device_fused=fused,
                **({"rabit_device_symmetric_heap": "160M"} if sym else {}))
     rank, world = rabit.get_rank(), rabit.get_world_size()
     dev = torch.device("cuda", 0)
-    sizes = (256 << 10, 1 << 20, 8 << 20, 32 << 20, 128 << 20)
+    sizes = (256 << 10, 1 << 20, 4 << 20, 16 << 20, 32 << 20, 128 << 20)
     if sym:
         sizes = (1 << 20, 8 << 20, 128 << 20)  # bump-allocated heap: keep the total small
     for nbytes in sizes:
@@ -59,6 +61,8 @@ def main():
         if rank == 0:
             print(json.dumps({
                 "world_on_one_gpu": world, "bytes": nbytes, "symmetric": sym, "t_us": round(med * 1e6, 1),
+                "fused": fused == "1", "fused_chunks": st.get("fused_chunks", 0),
+                "direct_push": st.get("direct_push", 0),
                 "phase_us": phase, "timed_ops": n1 - n0,
             }), flush=True)
         del x

@@ -25,7 +25,8 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python3 bench.py --steps 10 --warmup 3 ;;
-    multi) step multi 900 python -m pytest tests/test_gpu_multirank.py -x -q -p no:cacheprovider \
+    multi) step multi 900 python -u -m pytest tests/test_gpu_multirank.py -x -v -p no:cacheprovider \
+             --timeout 300 --timeout-method thread \
              -k "${MULTI_K:-}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kbench) step kbench 300 python tools/kernel_bench.py ;;
@@ -35,6 +36,17 @@ for s in $STEPS; do
              -d "$OUT/pmc" -o fetch -- python3 tools/kernel_bench.py --reps 3 --rounds 1 &&
          step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
              -d "$OUT/pmc" -o write -- python3 tools/kernel_bench.py --reps 3 --rounds 1 ;;
+    dbench)
+      # direct transport on ranks sharing the GPU: fused (one launch per chunk) vs classic
+      for w in 2 4; do
+        for mode in pull push; do
+          for f in 1 0; do
+            XR_FUSED=$f step dbench_w${w}_${mode}_f$f 300 python -m rabit_amd.launcher -n $w -- \
+              python tools/direct_bench.py rabit_device_direct_mode=$mode
+          done
+        done
+      done ;;
+    profw2) step profw2 400 bash tools/prof_world2.sh ;;
     speed) step speed 300 python -m rabit_amd.launcher -n 1 -- build/bin/speed_test 33554432 10 device=1 rabit_world1_fastpath=0 ;;
   esac
 done

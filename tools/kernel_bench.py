@@ -20,17 +20,22 @@ from rabit_amd import ops  # noqa: E402
 HBM_ROOF_TBPS = 6.3  # measured float4 copy on MI355X (MI355X_MICROARCH.md)
 
 
-def timeit(fn, reps):
+def timeit(fn, reps, inner):
+    """median / best GPU time of one call.  Each sample brackets `inner` back-to-back calls with
+    events: the host enqueues faster than the GPU drains them, so the per-call host overhead of
+    the Python / ctypes wrappers (which would otherwise sit between the start event and the
+    kernel) is hidden, for the rabit and the torch calls alike."""
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
     torch.cuda.synchronize()
     times = []
     for _ in range(reps):
         start.record()
-        fn()
+        for _ in range(inner):
+            fn()
         end.record()
         end.synchronize()
-        times.append(start.elapsed_time(end) * 1e-3)
+        times.append(start.elapsed_time(end) * 1e-3 / inner)
     times.sort()
     return times[len(times) // 2], times[0]
 
@@ -40,6 +45,7 @@ def main():
     ap.add_argument("--mb", type=int, default=128)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--inner", type=int, default=10, help="calls per timed sample")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = args.mb * (1 << 20) // 4
@@ -58,6 +64,7 @@ def main():
     bh = torch.rand(2 * n, generator=g, device=dev).to(torch.bfloat16)
     srcs_h = [torch.rand(n // 2, generator=g, device=dev).to(torch.bfloat16) for _ in range(8)]
     out_small_h = torch.empty(n // 2, device=dev, dtype=torch.bfloat16)
+    sums = torch.zeros(2, dtype=torch.int64, device=dev)
     cases = {
         "rabit_reduce_sum_f32": (lambda: ops.reduce_(a, b, ops.SUM), 3 * S),
         "torch_add_f32": (lambda: a.add_(b), 3 * S),
@@ -72,7 +79,8 @@ def main():
         "rabit_multi8_sum_f32": (lambda: ops.reduce_multi(out_small, srcs, ops.SUM), 9 * S // 4),
         "torch_stack_sum8_f32": (lambda: torch.sum(torch.stack(srcs), dim=0, out=out_small),
                                  9 * S // 4),
-        "rabit_checksum": (lambda: ops.checksum(a), S),
+        "rabit_checksum": (lambda: ops.checksum(a, out=sums), S),
+        "torch_sum_f32": (lambda: torch.sum(a), S),
         "rabit_reduce_sum_bf16": (lambda: ops.reduce_(ah, bh, ops.SUM), 3 * S),
         "torch_add_bf16": (lambda: ah.add_(bh), 3 * S),
         "rabit_multi8_sum_bf16": (lambda: ops.reduce_multi(out_small_h, srcs_h, ops.SUM), 9 * S // 4),
@@ -82,13 +90,14 @@ def main():
     results = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (fn, nbytes) in cases.items():
-            med, best = timeit(fn, args.reps)
+            med, best = timeit(fn, args.reps, args.inner)
             results[name].append((med, best, nbytes))
     for name, vals in results.items():
         med = sorted(v[0] for v in vals)[len(vals) // 2]
         best = min(v[1] for v in vals)
         nbytes = vals[0][2]
-        rec = {"kernel": name, "mib_per_operand": args.mb, "median_us": round(med * 1e6, 1),
+        rec = {"kernel": name, "mib_per_operand": args.mb, "inner": args.inner,
+               "median_us": round(med * 1e6, 1),
                "best_us": round(best * 1e6, 1), "GBps": round(nbytes / med / 1e9, 1),
                "pct_hbm_roof": round(100 * nbytes / med / 1e12 / HBM_ROOF_TBPS, 1)}
         print(json.dumps(rec), flush=True)
