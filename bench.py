@@ -198,7 +198,7 @@ def time_steps(rabit, torch, x, steps):
     return float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
 
 
-def run_variants(rabit, torch, dev, n, world, rank, ref, steps):
+def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=False):
     """every transport this job has up, on torch-allocated and symmetric-heap inputs: time
     and busbw of the 128 MiB float32 sum, each checked against the host fp64 reference"""
     out = []
@@ -231,7 +231,10 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps):
                 rec["busbw_GBps"] = round(n * 4 / t / 1e9 * 2 * (world - 1) / world, 2)
                 rabit.checkpoint(None)  # bounded result log
             out.append(rec)
-    # back to the calibrated choice of transport and direct form
+    # back to the calibrated choice of transport and direct form (or to RCCL after a fallback)
+    if forced_rccl:
+        rabit.set_device_transport(rabit.TRANSPORT_RCCL, None)
+        return out
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
     if st0.get("device_direct"):
         rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
@@ -297,9 +300,22 @@ def main():
     else:
         x = torch.empty(n, dtype=torch.float32, device=dev)
     checked = None
+    check_fallback = None
     if args.check:
         phase("check")
         checked = check_allreduce(rabit, x, rank, ref)
+        if not checked and world > 1:
+            # the calibrated transport returned a wrong result: say so, and time RCCL instead
+            # when it is up and correct (the same decision on every rank)
+            st0 = rabit.stats()
+            up = rabit.set_device_transport(rabit.TRANSPORT_RCCL, None)
+            up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
+            check_fallback = {"failed": "direct" if st0.get("device_direct") else "rccl",
+                              "direct_fused": bool(st0.get("direct_fused", 0)),
+                              "direct_push": bool(st0.get("direct_push", 0)),
+                              "now": "rccl" if up else None}
+            if up:
+                checked = check_allreduce(rabit, x, rank, ref)
         if not checked:
             raise SystemExit("allreduce result check against the host fp64 reference failed")
     g = torch.Generator(device=dev)
@@ -318,7 +334,8 @@ def main():
     if world > 1 and args.variants:
         phase("variants")
         rabit.checkpoint(None)
-        variants = run_variants(rabit, torch, dev, n, world, rank, ref, max(5, args.steps // 2))
+        variants = run_variants(rabit, torch, dev, n, world, rank, ref, max(5, args.steps // 2),
+                                forced_rccl=check_fallback is not None)
     phase("extras")
     extras = run_extras(rabit, torch, dev, world) if args.extras else {}
 
@@ -353,6 +370,7 @@ def main():
                             "busbw = algbw * 2(N-1)/N as nccl-tests",
         "baseline_note": "reference publishes no numbers (BASELINE.md)",
         "result_check": "bit-exact vs host fp64 reference" if checked else None,
+        "check_fallback": check_fallback,
         "consensus_elided": st.get("n_consensus_elided", 0),
         "device_epoch": st.get("device_epoch", 0),
         "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),

@@ -329,7 +329,9 @@ __global__ __launch_bounds__(kBlock) void CopyTileKernel(uint4 *__restrict__ dst
  * One 64-bit multiply per 16 bytes keeps it bandwidth-bound; order changes across vectors
  * and within a vector both change s2.
  */
-constexpr int kChecksumGrid = 2048;  // 8 workgroups per CU, tiles walked grid-stride
+constexpr int kChecksumGrid = 1024;  // 4 workgroups per CU, tiles walked grid-stride (measured
+                                     // best with 4 vectors per lane: tools/checksum_variants.hip)
+constexpr int kChecksumShards = 8;   // arrival counters, one 128-byte line each
 
 __device__ __forceinline__ void BlockSum2(unsigned long long &s1, unsigned long long &s2) {
 #pragma unroll
@@ -386,16 +388,37 @@ __global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint4 *__restrict
     }
   }
   BlockSum2(s1, s2);
+  // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): every partial is stored sc1
+  // (written through, agent scope) and drained (vmcnt(0)) before the same lane's agent-scope
+  // add to the counter of its shard (blockIdx % 8: one 128-byte line each, so 8 chains of
+  // ~grid/8 adds instead of one chain of grid adds: a single counter took 20 us at 2048
+  // workgroups).  The workgroup whose add completes its shard releases (agent fence) and adds
+  // to the top counter; the one that completes the top counter acquires and sums all partials.
   __shared__ bool last;
   if (threadIdx.x == 0) {
-    partial[2 * blockIdx.x] = s1;
-    partial[2 * blockIdx.x + 1] = s2;
-    __threadfence();  // the partial is visible before the arrival is counted
-    last = atomicAdd(arrived, 1u) == gridDim.x - 1;
+    __hip_atomic_store(&partial[2 * blockIdx.x], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&partial[2 * blockIdx.x + 1], s2, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned shard = blockIdx.x % kChecksumShards;
+    const unsigned members = (gridDim.x - shard + kChecksumShards - 1) / kChecksumShards;
+    const unsigned shards = gridDim.x < kChecksumShards ? gridDim.x : kChecksumShards;
+    bool top = false;
+    if (__hip_atomic_fetch_add(arrived + shard * 32, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      top = __hip_atomic_fetch_add(arrived + kChecksumShards * 32, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == shards - 1;
+      if (top) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    last = top;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire: every other workgroup's partial
   s1 = s2 = 0;
   for (unsigned i = threadIdx.x; i < gridDim.x; i += kBlock) {
     s1 += __hip_atomic_load(&partial[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -405,7 +428,10 @@ __global__ __launch_bounds__(kBlock) void ChecksumKernel(const uint4 *__restrict
   if (threadIdx.x == 0) {
     out[0] += s1;
     out[1] += s2;
-    *arrived = 0;  // re-armed for the next launch on this device (stream order)
+    // re-armed for the next launch on this device (stream order)
+    for (int k = 0; k <= kChecksumShards; ++k) {
+      __hip_atomic_store(arrived + k * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -544,7 +570,8 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
     auto it = scratch.find(dev);
     if (it == scratch.end()) {
       void *p = nullptr;
-      const size_t bytes = sizeof(unsigned long long) * (2 * kChecksumGrid + 1);
+      const size_t bytes =
+          sizeof(unsigned long long) * 2 * kChecksumGrid + 128 * (kChecksumShards + 1);
       e = hipMalloc(&p, bytes);
       if (e != hipSuccess) return e;
       e = hipMemset(p, 0, bytes);

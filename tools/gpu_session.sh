@@ -28,10 +28,12 @@ for s in $STEPS; do
     multi) step multi 900 python -u -m pytest tests/test_gpu_multirank.py -x -v -p no:cacheprovider \
              --timeout 300 --timeout-method thread \
              -k "${MULTI_K:-}" ;;
+    ktests) step ktests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -p no:cacheprovider \
+             --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kbench) step kbench 300 python tools/kernel_bench.py ;;
     kprof) step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$OUT/kprof" -o kbench -- python3 tools/kernel_bench.py --reps 5 --rounds 1 ;;
+             -d "$OUT/kprof" -o kbench -- python3 tools/kernel_bench.py --reps 5 --rounds 1 --inner 2 ;;
     pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv \
              -d "$OUT/pmc" -o fetch -- python3 tools/kernel_bench.py --reps 3 --rounds 1 &&
          step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \

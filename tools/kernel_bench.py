@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--inner", type=int, default=10, help="calls per timed sample")
+    ap.add_argument("--only", default="", help="comma-separated substrings of kernel names")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = args.mb * (1 << 20) // 4
@@ -87,6 +88,9 @@ def main():
         "torch_stack_sum8_bf16": (lambda: torch.sum(torch.stack(srcs_h), dim=0, out=out_small_h),
                                   9 * S // 4),
     }
+    if args.only:
+        keys = args.only.split(",")
+        cases = {k: v for k, v in cases.items() if any(q in k for q in keys)}
     results = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (fn, nbytes) in cases.items():
