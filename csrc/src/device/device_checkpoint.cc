@@ -27,10 +27,10 @@ DeviceCheckpoint::~DeviceCheckpoint() {
   (void)hipStreamSynchronize(side_);
   for (auto &h : half_) {
     for (void *p : h.dev) (void)hipFree(p);
-    if (h.pinned != nullptr) (void)hipHostFree(h.pinned);
     (void)hipEventDestroy(h.d2h_done);
     (void)hipEventDestroy(h.snap_done);
   }
+  if (pinned_ != nullptr) (void)hipHostFree(pinned_);
   (void)hipStreamDestroy(side_);
 }
 
@@ -44,29 +44,28 @@ size_t DeviceCheckpoint::reserved_bytes() const {
 
 const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const size_t *nbytes,
                                                const std::string &meta) {
-  // the oldest slot: the newest two versions stay intact
-  cur_ = (cur_ + 1) % kSlots;
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) total += nbytes[i];
+  if (nslots_ == 0) {
+    nslots_ = slots_req_ == 2 || slots_req_ == 3 ? slots_req_
+                                                 : (total < three_slot_max_ ? 3 : 2);
+  }
+  // the oldest slot: the newest version (and, with 3 slots, the one before) stays intact
+  cur_ = (cur_ + 1) % nslots_;
   Half &h = half_[cur_];
   // a mirror still reading this slot must finish before its buffers are reused
   CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
+  if (pinned_owner_ == &h) pinned_owner_ = nullptr;  // its bytes are about to change
   h.dev.resize(n, nullptr);
   h.cap.resize(n, 0);
   h.sizes.assign(nbytes, nbytes + n);
   h.meta = meta;
-  size_t total = 0;
   for (int i = 0; i < n; ++i) {
     if (h.cap[i] < nbytes[i]) {
       if (h.dev[i] != nullptr) (void)hipFree(h.dev[i]);
       CheckHip(hipMalloc(&h.dev[i], std::max<size_t>(nbytes[i], 256)), "hipMalloc(snapshot)");
       h.cap[i] = std::max<size_t>(nbytes[i], 256);
     }
-    total += nbytes[i];
-  }
-  if (h.pinned_cap < total) {
-    if (h.pinned != nullptr) (void)hipHostFree(h.pinned);
-    CheckHip(hipHostMalloc(reinterpret_cast<void **>(&h.pinned), std::max<size_t>(total, 1)),
-             "hipHostMalloc(mirror)");
-    h.pinned_cap = std::max<size_t>(total, 1);
   }
   // 1. HBM snapshot on the plane stream, ordered after the caller's stream
   plane_->EnterFromUser();
@@ -75,14 +74,13 @@ const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const s
   // the caller may overwrite its tensors only after the snapshot read them
   plane_->Finish(FailureProbe(), false);
   // 2. pinned host mirror on the side stream: always, or when the previous one is done
-  h.mirror_valid = false;
   bool idle = last_mirror_ == nullptr;
   if (!idle) {
     const hipError_t q = hipEventQuery(last_mirror_->d2h_done);
     if (q != hipErrorNotReady) CheckHip(q, "checkpoint mirror query");
     idle = q == hipSuccess;
   }
-  if (mirror_always_ || idle) {
+  if (mirror_mode_ == kMirrorAlways || (mirror_mode_ == kMirrorIdle && idle)) {
     h.StartMirror();
     mirrors_ += 1;
   } else {
@@ -92,22 +90,37 @@ const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const s
 }
 
 void DeviceCheckpoint::Half::StartMirror() const {
-  CheckHip(hipStreamWaitEvent(owner->side_, snap_done, 0), "hipStreamWaitEvent(mirror)");
+  DeviceCheckpoint *o = owner;
+  size_t total = 0;
+  for (size_t s : sizes) total += s;
+  if (o->pinned_cap_ < total) {
+    // the side stream holds the only readers and writers of the old buffer
+    CheckHip(hipStreamSynchronize(o->side_), "checkpoint mirror drain");
+    if (o->pinned_ != nullptr) (void)hipHostFree(o->pinned_);
+    o->pinned_ = nullptr;
+    o->pinned_cap_ = 0;
+    CheckHip(hipHostMalloc(reinterpret_cast<void **>(&o->pinned_), std::max<size_t>(total, 1)),
+             "hipHostMalloc(mirror)");
+    o->pinned_cap_ = std::max<size_t>(total, 1);
+  }
+  // queued behind any earlier mirror on the same stream, so copies into the shared buffer
+  // never overlap
+  CheckHip(hipStreamWaitEvent(o->side_, snap_done, 0), "hipStreamWaitEvent(mirror)");
   size_t off = 0;
   for (size_t i = 0; i < sizes.size(); ++i) {
     if (sizes[i] != 0) {
-      CheckHip(hipMemcpyAsync(pinned + off, dev[i], sizes[i], hipMemcpyDeviceToHost, owner->side_),
+      CheckHip(hipMemcpyAsync(o->pinned_ + off, dev[i], sizes[i], hipMemcpyDeviceToHost, o->side_),
                "D2H mirror");
     }
     off += sizes[i];
   }
-  CheckHip(hipEventRecord(d2h_done, owner->side_), "hipEventRecord(mirror)");
-  mirror_valid = true;
-  owner->last_mirror_ = this;
+  CheckHip(hipEventRecord(d2h_done, o->side_), "hipEventRecord(mirror)");
+  o->pinned_owner_ = this;
+  o->last_mirror_ = this;
 }
 
 void DeviceCheckpoint::Half::Save(Stream *fo) const {
-  if (!mirror_valid) StartMirror();  // deferred mirror: a peer needs the bytes now
+  if (!mirrored()) StartMirror();  // deferred mirror: a peer needs the bytes now
   CheckHip(hipEventSynchronize(d2h_done), "checkpoint mirror wait");
   uint64_t ml = meta.size();
   fo->Write(&ml, sizeof(ml));
@@ -120,7 +133,7 @@ void DeviceCheckpoint::Half::Save(Stream *fo) const {
   }
   size_t total = 0;
   for (size_t s : sizes) total += s;
-  if (total != 0) fo->Write(pinned, total);
+  if (total != 0) fo->Write(owner->pinned_, total);
 }
 
 void DeviceCheckpoint::Half::Load(Stream *) { utils::Error("snapshot halves are save-only"); }

@@ -6,15 +6,19 @@
  * device tensors that means a synchronous D2H of the whole model on the critical path.  Here
  * a checkpoint is:
  *   1. an HBM-to-HBM snapshot of the tensors (gfx950 copy kernel, ~6 TB/s) into the oldest of
- *      kSlots snapshot slots (the previous version must stay intact until the new checkpoint
- *      is acknowledged, peers may still be loading it; a third slot lets a host mirror still
- *      be in flight),
- *   2. an asynchronous D2H copy of the snapshot into pinned host memory on a side stream
+ *      2 or 3 snapshot slots.  Two are required: the previous version must stay intact until
+ *      the new checkpoint is acknowledged (peers may still be loading it) — the same 2x model
+ *      size the reference holds while it serialises a new checkpoint next to the old one.  A
+ *      third slot lets the host mirror of a slot still be in flight when that slot comes round
+ *      again; it is used for models below rabit_device_ckpt_3slot_max (default 4 GiB), where a
+ *      third copy is cheap and checkpoints may come faster than a PCIe copy of the model;
+ *      rabit_device_ckpt_slots=2|3 forces either,
+ *   2. an asynchronous D2H copy of the snapshot into ONE pinned host buffer on a side stream
  *      (overlaps the next iterations; host-DRAM durability).  In the default "idle" mode a
  *      mirror starts only when the previous one has finished, so iterations shorter than a
  *      PCIe copy of the model are never throttled by it; a snapshot that was not mirrored is
- *      copied on demand if a peer asks for its bytes.  "always" mirrors every checkpoint
- *      (rabit_device_ckpt_mirror=always),
+ *      copied on demand if a peer asks for its bytes.  "always" mirrors every checkpoint,
+ *      "off" only on demand (rabit_device_ckpt_mirror=always|idle|off),
  *   3. registration with the robust engine as a *lazy* checkpoint: bytes are produced (from the
  *      pinned mirror, after its event) only if a recovering peer requests them.
  * Wire format of the global checkpoint: uint64 meta_len, meta, uint64 n, n x uint64 size,
@@ -58,8 +62,17 @@ class DeviceCheckpoint {
     }
     return false;
   }
-  /*! \brief mirror policy: true = every checkpoint, false = when the side stream is idle */
-  void set_mirror_always(bool v) { mirror_always_ = v; }
+  /*! \brief mirror policy */
+  enum MirrorMode { kMirrorIdle = 0, kMirrorAlways = 1, kMirrorOff = 2 };
+  void set_mirror_mode(int m) { mirror_mode_ = m; }
+  /*! \brief snapshot slots: 2, 3, or 0 = by size (3 below three_slot_max bytes) */
+  void set_slots(int n, size_t three_slot_max) {
+    slots_req_ = n;
+    three_slot_max_ = three_slot_max;
+  }
+  int slots() const { return nslots_; }
+  /*! \brief bytes of pinned host memory held by the mirror */
+  size_t pinned_bytes() const { return pinned_cap_; }
   /*! \brief checkpoints whose host mirror was started at snapshot time / deferred */
   uint64_t mirrors() const { return mirrors_; }
   uint64_t mirrors_deferred() const { return mirrors_deferred_; }
@@ -83,13 +96,12 @@ class DeviceCheckpoint {
     std::vector<size_t> cap;      // their capacities
     std::vector<size_t> sizes;    // payload sizes of the current snapshot
     std::string meta;
-    char *pinned{nullptr};        // pinned host mirror
-    size_t pinned_cap{0};
     hipEvent_t d2h_done{nullptr};
     hipEvent_t snap_done{nullptr};  // the HBM snapshot of this slot is complete
-    mutable bool mirror_valid{false};  // pinned holds this snapshot (or its copy is queued)
-    /*! \brief queue the D2H mirror of this slot on the side stream */
+    /*! \brief queue the D2H mirror of this slot into the shared pinned buffer (side stream) */
     void StartMirror() const;
+    /*! \brief the pinned buffer holds this slot's current snapshot (or its copy is queued) */
+    bool mirrored() const { return owner->pinned_owner_ == this; }
     void Load(Stream *) override;
     void Save(Stream *fo) const override;
   };
@@ -104,8 +116,14 @@ class DeviceCheckpoint {
   hipStream_t side_{nullptr};
   static constexpr int kSlots = 3;
   Half half_[kSlots];
-  int cur_{kSlots - 1};
-  bool mirror_always_{false};
+  int nslots_{0};  // fixed at the first snapshot
+  int slots_req_{0};
+  size_t three_slot_max_{size_t(4) << 30};
+  int cur_{-1};
+  int mirror_mode_{kMirrorIdle};
+  char *pinned_{nullptr};  // the host mirror, shared by the slots
+  size_t pinned_cap_{0};
+  const Half *pinned_owner_{nullptr};
   const Half *last_mirror_{nullptr};  // slot of the most recently started mirror
   uint64_t mirrors_{0}, mirrors_deferred_{0};
   LoaderImpl loader_;

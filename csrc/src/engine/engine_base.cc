@@ -124,13 +124,22 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_host_shm")) shm_enabled_ = utils::StringToBool(val);
   if (is("rabit_device_ckpt_mirror")) {
     if (!strcmp(val, "always")) {
-      ckpt_mirror_always_ = true;
+      ckpt_mirror_mode_ = device::DeviceCheckpoint::kMirrorAlways;
     } else if (!strcmp(val, "idle")) {
-      ckpt_mirror_always_ = false;
+      ckpt_mirror_mode_ = device::DeviceCheckpoint::kMirrorIdle;
+    } else if (!strcmp(val, "off")) {
+      ckpt_mirror_mode_ = device::DeviceCheckpoint::kMirrorOff;
     } else {
-      utils::Error("rabit_device_ckpt_mirror must be always or idle (got %s)", val);
+      utils::Error("rabit_device_ckpt_mirror must be always, idle or off (got %s)", val);
     }
   }
+  if (is("rabit_device_ckpt_slots")) {
+    ckpt_slots_ = atoi(val);
+    utils::Check(ckpt_slots_ == 0 || ckpt_slots_ == 2 || ckpt_slots_ == 3,
+                 "rabit_device_ckpt_slots must be 2, 3 or 0 (by size)");
+  }
+  if (is("rabit_device_ckpt_3slot_max")) ckpt_3slot_max_ = core::ParseUnit(name, val);
+
   if (is("rabit_host_shm_min")) shm_min_ = core::ParseUnit(name, val);
   if (is("rabit_host_shm_buffer")) shm_stage_ = core::ParseUnit(name, val);
   if (is("rabit_poll_interval_ms")) hcfg_.poll_interval_ms = std::max(1, atoi(val));
@@ -848,7 +857,8 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
   device::DeviceGuard dg(dev_->device());
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
-    dev_ckpt_->set_mirror_always(ckpt_mirror_always_);
+    dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
+    dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
   trace::Scope ts("device_snapshot", rank_, version_number_, seq_counter_, 0, 1);
   const Serializable *snap = dev_ckpt_->Snapshot(n, ptrs, nbytes, meta);
@@ -867,7 +877,8 @@ int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes
   device::DeviceGuard dg(dev_->device());
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
-    dev_ckpt_->set_mirror_always(ckpt_mirror_always_);
+    dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
+    dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
   dev_local_.owner = this;
   dev_local_.Set(nl, lptrs, lnbytes);
@@ -942,7 +953,11 @@ std::string EngineBase::StatsJson() const {
      << ",\"n_allgather\":" << s.n_allgather << ",\"n_checkpoint\":" << s.n_checkpoint
      << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_shm_ops\":" << s.n_shm_ops
      << ",\"ckpt_mirrors\":" << (dev_ckpt_ ? dev_ckpt_->mirrors() : 0)
-     << ",\"ckpt_mirrors_deferred\":" << (dev_ckpt_ ? dev_ckpt_->mirrors_deferred() : 0) << ",\"n_recovered_ops\":" << s.n_recovered_ops
+     << ",\"ckpt_mirrors_deferred\":" << (dev_ckpt_ ? dev_ckpt_->mirrors_deferred() : 0)
+     << ",\"ckpt_slots\":" << (dev_ckpt_ ? dev_ckpt_->slots() : 0)
+     << ",\"ckpt_hbm_bytes\":" << (dev_ckpt_ ? dev_ckpt_->reserved_bytes() : 0)
+     << ",\"ckpt_pinned_bytes\":" << (dev_ckpt_ ? dev_ckpt_->pinned_bytes() : 0)
+     << ",\"n_recovered_ops\":" << s.n_recovered_ops
      << ",\"n_recover_events\":" << s.n_recover_events << ",\"n_consensus\":" << s.n_consensus
      << ",\"n_consensus_elided\":" << s.n_consensus_elided
      << ",\"n_device_replays\":" << s.n_device_replays

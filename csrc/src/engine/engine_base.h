@@ -226,7 +226,9 @@ class EngineBase : public IEngine {
   // one-peer direct group) instead of the local short-cut, so their API paths run on one GPU
   bool world1_transport_{false};
   bool shm_enabled_{true};          // rabit_host_shm
-  bool ckpt_mirror_always_{false};  // rabit_device_ckpt_mirror=always: mirror every checkpoint
+  int ckpt_mirror_mode_{0};          // rabit_device_ckpt_mirror: 0 idle, 1 always, 2 off
+  int ckpt_slots_{0};                // rabit_device_ckpt_slots: 2, 3, 0 = by size
+  size_t ckpt_3slot_max_{size_t(4) << 30};  // by size: 3 slots below this many bytes
   size_t shm_min_{1u << 20};        // rabit_host_shm_min
   size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)
   bool calibrate_{true};

@@ -38,5 +38,7 @@ for it in range(4):
 torch.cuda.synchronize()
 assert torch.all(w == wv), (float(w[0]), wv)
 assert torch.all(b == 4.5)
+st = rabit.stats()
 rabit.finalize()
-print("[%d] DEVCKPT OK" % rank, flush=True)
+print("[%d] DEVCKPT OK slots=%d hbm=%d pinned=%d" % (rank, st["ckpt_slots"], st["ckpt_hbm_bytes"],
+                                                   st["ckpt_pinned_bytes"]), flush=True)

@@ -30,3 +30,27 @@ def test_device_checkpoint_recovery(mock):
         import re
         loads = [int(x) for x in re.findall(r"device loads (\d+)", out)]
         assert loads and min(loads) >= 1, out[-3000:]
+
+
+@pytest.mark.parametrize("replay", ["1", "0"])
+def test_device_checkpoint_recovery_two_slots(replay):
+    """the lean layout: 2 HBM snapshot slots (2x model, as the reference's old + new copy) and
+    no proactive host mirror; replay=0 serves the restarted rank over TCP, so the survivor's
+    shared pinned buffer is filled on demand from the acknowledged slot"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import re
+    script = os.path.join(ROOT, "tests", "scripts", "device_ckpt_recover.py")
+    job = LocalJob([sys.executable, script, "mock=0,1,0,0", "mock=2,3,1,0",
+                    "rabit_device_ckpt_slots=2", "rabit_device_ckpt_mirror=off",
+                    "rabit_device_replay=" + replay], 3, 4, capture=True, timeout=240,
+                   print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-4000:]
+    assert out.count("DEVCKPT OK") == 3, out[-3000:]
+    assert "reloaded version" in out
+    assert set(re.findall(r"slots=(\d+)", out)) == {"2"}, out[-3000:]
+    # two slots of (64 Ki floats + 7 doubles) each, 256-byte rounded
+    hbm = [int(x) for x in re.findall(r"hbm=(\d+)", out)]
+    assert max(hbm) <= 2 * ((1 << 18) + 256), hbm
