@@ -50,7 +50,9 @@ def test_device_checkpoint_recovery_two_slots(replay):
     assert rc == 0, out[-4000:]
     assert out.count("DEVCKPT OK") == 3, out[-3000:]
     assert "reloaded version" in out
-    assert set(re.findall(r"slots=(\d+)", out)) == {"2"}, out[-3000:]
+    # (a rank restarted after the last checkpoint never snapshots again: 0 slots)
+    slots = set(re.findall(r"slots=(\d+)", out))
+    assert "2" in slots and slots <= {"0", "2"}, out[-3000:]
     # two slots of (64 Ki floats + 7 doubles) each, 256-byte rounded
     hbm = [int(x) for x in re.findall(r"hbm=(\d+)", out)]
     assert max(hbm) <= 2 * ((1 << 18) + 256), hbm
