@@ -240,10 +240,16 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
   ncclUniqueId id;
   std::memcpy(id.internal, id_bytes.data(), sizeof(id.internal));
   CheckHip(hipSetDevice(device_), "hipSetDevice");
-  ncclResult_t r = ncclCommInitRank(&comm_, nranks, id, rank);
+  // channel (CTA) bounds for the 7 xGMI links: RCCL's own choice unless configured
+  // (rabit_rccl_min_ctas / rabit_rccl_max_ctas; one CTA drives one channel)
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  if (cfg_.rccl_min_ctas > 0) config.minCTAs = cfg_.rccl_min_ctas;
+  if (cfg_.rccl_max_ctas > 0) config.maxCTAs = cfg_.rccl_max_ctas;
+  config.commName = "xrabit";
+  ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &config);
   if (r != ncclSuccess) {
     comm_ = nullptr;
-    utils::HandleLogInfo("[xrabit] ncclCommInitRank failed: %s\n", ncclGetErrorString(r));
+    utils::HandleLogInfo("[xrabit] ncclCommInitRankConfig failed: %s\n", ncclGetErrorString(r));
     return Status::kAborted;
   }
   nranks_ = nranks;

@@ -60,6 +60,8 @@ struct DeviceConfig {
                                        // 1 always, 2 as the calibration finds faster
   int fused_grid{0};                   // workgroups of a fused launch (0: automatic)
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
+  int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
+  int rccl_max_ctas{0};
 };
 
 /*! \brief exit status of a rank whose own device stream stayed wedged after an abort (the

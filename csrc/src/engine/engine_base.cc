@@ -103,6 +103,8 @@ void EngineBase::SetParam(const char *name, const char *val) {
     dcfg_.fused_mode = !strcmp(val, "auto") ? 2 : (utils::StringToBool(val) ? 1 : 0);
   }
   if (is("rabit_device_fused_grid")) dcfg_.fused_grid = atoi(val);
+  if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
+  if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
     if (!strcmp(val, "auto")) {

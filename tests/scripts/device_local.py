@@ -8,14 +8,21 @@ the replicas of its rabit_local_replica ring predecessors in HBM and replicates 
 device copies.  The mock engine kills ranks (`mock=rank,version,seq,trial`; seq 1 is the
 checkpoint call); a restarted rank must get back its own local tensors bit for bit, which is
 checked against their closed form right after the load and at the end."""
+import os
 import sys
 
 import torch
 
 import rabit_amd as rabit
 
-rabit.init(sys.argv[1:], lib="mock", rabit_device=0, rabit_device_peer_buffer="1M",
-           rabit_device_peer_timeout_sec=20)
+ctx = None
+params = dict(rabit_device=0, rabit_device_peer_buffer="1M", rabit_device_peer_timeout_sec=20)
+if os.environ.get("XR_ENV_INIT") == "1":
+    # ranks started one by one (e.g. each under its own profiler, tools/prof_local.sh)
+    from rabit_amd.torchrun import init_from_env
+    ctx = init_from_env(lib="mock", **params)
+else:
+    rabit.init(sys.argv[1:], lib="mock", **params)
 rank, world = rabit.get_rank(), rabit.get_world_size()
 dev = torch.device("cuda", 0)
 N = (1 << 16) + 5
@@ -58,6 +65,9 @@ assert torch.all(w == expect), (float(w[0]), expect)
 el, es = local_expect(ITERS)
 assert torch.equal(loc.cpu(), el) and torch.equal(steps.cpu(), es)
 st = rabit.stats()
-rabit.finalize()
+if ctx is not None:
+    ctx.finalize()
+else:
+    rabit.finalize()
 print("[%d] DEVLOCAL OK bytes_local_in=%d recovered=%d" %
       (rank, int(st["bytes_local_in"]), st["n_recovered_ops"]), flush=True)

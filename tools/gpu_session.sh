@@ -49,6 +49,7 @@ for s in $STEPS; do
         done
       done ;;
     profw2) step profw2 400 bash tools/prof_world2.sh ;;
+    proflocal) step proflocal 300 bash tools/prof_local.sh ;;
     speed) step speed 300 python -m rabit_amd.launcher -n 1 -- build/bin/speed_test 33554432 10 device=1 rabit_world1_fastpath=0 ;;
   esac
 done
