@@ -357,6 +357,17 @@ bool DevicePlane::Preflight(const std::vector<PeerRecord> &all, int rank, std::s
         *why = "GPU " + std::to_string(device_) + " cannot access the GPU of rank " +
                std::to_string(r) + " (" + pci + ")";
       }
+      if (li.can_access == 1) {
+        // kernels of this process read and write the peer's mapped buffers directly (the IPC
+        // mapping's lazy flag covers the same; enabling it here makes the order explicit)
+        DeviceGuard dg(device_);
+        const hipError_t e = hipDeviceEnablePeerAccess(li.ordinal, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          utils::HandleLogInfo("[xrabit] hipDeviceEnablePeerAccess(%d -> %d): %s\n", device_,
+                               li.ordinal, hipGetErrorString(e));
+        }
+        (void)hipGetLastError();
+      }
     }
     links_.push_back(li);
   }

@@ -145,6 +145,8 @@ class DevicePlane {
   DeviceArena *spill_arena() { return cfg_.spill_cap != 0 ? &spill_ : nullptr; }
   /*! \brief scratch slot staging spilled results (HBM side of the D2H / H2D copies) */
   static constexpr int kSpillScratch = 3;
+  /*! \brief scratch slot of the calibration's second destination */
+  static constexpr int kCalibScratch = 4;
   const DeviceConfig &config() const { return cfg_; }
 
   // ---- communicator lifecycle
@@ -321,10 +323,11 @@ class DevicePlane {
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};
   size_t pending_bytes_{0};
-  // 0/1: all-to-all path, 2: host-buffer staging, 3: spilled results
-  static constexpr int kScratchSlots = 4;
-  void *scratch_[kScratchSlots]{nullptr, nullptr, nullptr, nullptr};
-  size_t scratch_bytes_[kScratchSlots]{0, 0, 0, 0};
+  // 0/1: all-to-all path (and calibration), 2: host-buffer staging, 3: spilled results,
+  // 4: calibration second destination
+  static constexpr int kScratchSlots = 5;
+  void *scratch_[kScratchSlots]{};
+  size_t scratch_bytes_[kScratchSlots]{};
   void *pinned_{nullptr};
   size_t pinned_bytes_{0};
   size_t op_bytes_{0};

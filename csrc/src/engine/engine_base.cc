@@ -425,6 +425,10 @@ Status EngineBase::CalibrateDevice() {
   float *src = heap_src ? reinterpret_cast<float *>(heap.base + dev_->sym_heap_used())
                         : static_cast<float *>(dev_->Scratch(sizes[1] * 4, 0));
   float *dst = static_cast<float *>(dev_->Scratch(sizes[1] * 4, 1));
+  // the robust engine stores every device result twice (result log + user buffer): the direct
+  // kernels do it in the same pass, RCCL needs a copy after the collective.  Time what the
+  // engine runs, both destinations and the copy included.
+  float *dst2 = static_cast<float *>(dev_->Scratch(sizes[1] * 4, device::DevicePlane::kCalibScratch));
   const int n = GetWorldSize();
   double t[2][2] = {{0, 0}, {0, 0}};  // [transport: 0 rccl, 1 direct][size]
   int ok = 1;
@@ -449,10 +453,11 @@ Status EngineBase::CalibrateDevice() {
       *st = dev_->Finish(MakeProbe());
       if (*st != Status::kSuccess) return false;
       const double t0 = utils::GetTime();
-      *st = dev_->Allreduce(src, dst, nullptr, count, mpi::kFloat, mpi::kSum, device::kPrepCopy,
+      *st = dev_->Allreduce(src, dst, dst2, count, mpi::kFloat, mpi::kSum, device::kPrepCopy,
                             1.0, MakeProbe());
       if (*st == Status::kSuccess) *st = dev_->Finish(MakeProbe());
       if (*st != Status::kSuccess) return false;
+      dev_->Synchronize();  // the second destination's copy (RCCL) is part of the op
       if (rep > 0) best = std::min(best, utils::GetTime() - t0);
     }
     t[which][k] = best;
