@@ -42,12 +42,16 @@ def test_direct_collectives_push(world):
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("mock", [[], ["mock=1,1,0,0"], ["mock=0,2,1,0", "mock=2,1,2,0"]])
 @pytest.mark.parametrize("mode", ["pull", "push"])
-def test_direct_recovery(mock, mode):
+def test_direct_recovery(mock, mode, fused):
+    """kills at fixed points, both forms of the two-shot path (fused=1: the survivors' fused
+    kernels give up on the abort word, the guard word keeps later launches of the group idle)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("device_ft.py", 3, mock + ["rabit_device_direct_mode=" + mode], attempts=4)
+    rc, out = _run("device_ft.py", 3, mock + ["rabit_device_direct_mode=" + mode,
+                                              "rabit_device_fused=" + fused], attempts=4)
     assert rc == 0, out[-5000:]
     assert out.count("DEVFT OK") == 3, out[-3000:]
     if mock:
@@ -179,8 +183,9 @@ def test_device_local_checkpoint_recovery(extra):
     assert all(g > 0 for g in got), got
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("mode", ["pull", "push"])
-def test_device_hang_detected_and_recovered(mode):
+def test_device_hang_detected_and_recovered(mode, fused):
     """mock_dev_hang: rank 1 stays alive but its GPU stream wedges right before a device
     allreduce.  The survivors' barriers give up, they abort and re-link; rank 1 finds its own
     stream still stuck after the abort and exits for a restart; the job finishes with the
@@ -188,7 +193,8 @@ def test_device_hang_detected_and_recovered(mode):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     rc, out = _run("device_ft.py", 3, ["mock_dev_hang=1,1,0,0", "rabit_device_drain_timeout_sec=5",
-                                       "rabit_device_direct_mode=" + mode], attempts=3, timeout=240)
+                                       "rabit_device_direct_mode=" + mode,
+                                       "rabit_device_fused=" + fused], attempts=3, timeout=240)
     assert rc == 0, out[-5000:]
     assert out.count("DEVFT OK") == 3, out[-3000:]
     assert "Hit Mock Device Hang" in out and "device stream wedged" in out, out[-3000:]
