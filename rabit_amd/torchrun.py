@@ -92,6 +92,12 @@ def init_from_env(lib: str = "standard", port_offset: int = TRACKER_PORT_OFFSET,
         # can uniformly take the HBM transports (staged over PCIe) instead of loopback TCP
         params["rabit_host_via_device"] = 1
     args.update(params)
+    # extra engine parameters for every rank of a launched job: XRABIT_PARAMS="k=v,k=v"
+    # (rehearsals and tuning runs; explicit keyword parameters win)
+    for kv in filter(None, os.environ.get("XRABIT_PARAMS", "").split(",")):
+        k, _, v = kv.partition("=")
+        if k and k not in params:
+            args[k.strip()] = v.strip()
     rabit.init(lib=lib, **args)
     assert rabit.get_world_size() == world, "rabit world size differs from torchrun's"
     return TorchrunContext(rank, world, local_rank, tracker)

@@ -16,5 +16,7 @@ rabit.allreduce(x, rabit.SUM)
 assert torch.all(x == ctx.world * (ctx.world + 1) / 2)
 t = np.array([float(ctx.rank)])
 assert rabit.allreduce(t, rabit.MAX)[0] == ctx.world - 1
-print("TORCHRUN OK rank=%d" % ctx.rank, flush=True)
+for _ in range(3):
+    rabit.allreduce(np.ones(4), rabit.SUM)
+print("TORCHRUN OK rank=%d elided=%d" % (ctx.rank, rabit.stats()["n_consensus_elided"]), flush=True)
 ctx.finalize()
