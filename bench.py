@@ -284,8 +284,8 @@ def main():
     shared_gpu = ngpu < int(os.environ.get("LOCAL_WORLD_SIZE", world))
     torch.cuda.set_device(gpu)
     n = args.size_mb * (1 << 20) // 4
-    # the symmetric heap holds the variant matrix's second buffer (+ 48 MiB: the calibration's
-    # 32 MiB inputs come from the heap's free tail when it has one)
+    # the symmetric heap holds the variant matrix's second buffer (+ 48 MiB of slack); the
+    # calibration runs first and reads its inputs (up to 128 MiB) from the heap's free tail
     heap_bytes = n * 4 + (48 << 20) if (world > 1 and args.variants) or args.symmetric else 0
     heap = {"rabit_device_symmetric_heap": str(heap_bytes)} if heap_bytes else {}
     phase("init")

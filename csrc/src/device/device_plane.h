@@ -60,6 +60,7 @@ struct DeviceConfig {
                                        // 1 always, 2 as the calibration finds faster
   int fused_grid{0};                   // workgroups of a fused launch (0: automatic)
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
+  size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
   int rccl_max_ctas{0};
 };

@@ -104,6 +104,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   }
   if (is("rabit_device_fused_grid")) dcfg_.fused_grid = atoi(val);
   if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
+  if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
@@ -414,7 +415,11 @@ Status EngineBase::EnsureDeviceComm() {
 
 Status EngineBase::CalibrateDevice() {
   // sizes in float32 elements; every rank runs the same sequence (this is a collective)
-  const size_t big = std::min<size_t>(32u << 20, dev_->has_peers() ? dcfg_.peer_stage : 0) / 4;
+  // the large point sits where gradient buckets and the headline op live: 128 MiB (one stage
+  // chunk at most); on 8 ranks sharing a GPU the fastest form at 32 MiB was not the fastest
+  // at 128 MiB (profiles/r2_s5_rehearsal_n8)
+  const size_t big =
+      std::min<size_t>(dcfg_.calib_big, dev_->has_peers() ? dcfg_.peer_stage : 0) / 4;
   const size_t sizes[2] = {64u << 10, std::max<size_t>(big, 1u << 20)};
   // Inputs come from the free tail of the symmetric heap when the job has one: its buffers
   // live there, and the calibration then times the paths they take (the direct transport reads
