@@ -273,6 +273,13 @@ void DevicePlane::AbortComm() {
   peers_.reset();
 }
 
+void DevicePlane::DropComm() {
+  if (comm_ != nullptr) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
 void DevicePlane::InjectHang(double max_sec) {
   int *w = g_hang_release.load();
   if (w == nullptr) {

@@ -157,6 +157,8 @@ class DevicePlane {
   Status InitComm(const std::string &id, int nranks, int rank, const FailureProbe &probe);
   /*! \brief abort the communicator and the peer group (unblocks in-flight kernels), drop them */
   void AbortComm();
+  /*! \brief drop the RCCL communicator alone (no op in flight on it), keep the peer group */
+  void DropComm();
   bool has_comm() const { return comm_ != nullptr; }
   bool has_peers() const { return peers_ != nullptr; }
   /*! \brief a transport for world > 1 is up */

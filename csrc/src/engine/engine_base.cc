@@ -124,6 +124,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
   if (is("rabit_host_out_of_place")) host_out_of_place_ = utils::StringToBool(val);
   if (is("rabit_device_world1_transport")) world1_transport_ = utils::StringToBool(val);
+  if (is("rabit_mock_rccl_init_fail")) mock_rccl_fail_ = utils::StringToBool(val);
   if (is("rabit_host_shm")) shm_enabled_ = utils::StringToBool(val);
   if (is("rabit_device_ckpt_mirror")) {
     if (!strcmp(val, "always")) {
@@ -386,14 +387,37 @@ Status EngineBase::EnsureDeviceComm() {
   if (s != Status::kSuccess) return s;
   if (!ok) dev_->DropPeers();
   // 3. RCCL: RCCL refuses several ranks on one GPU, which the direct transport handles alone
-  const bool want_rccl = dcfg_.algo != 2 && !dup_gpu;
+  // (test hook rabit_mock_rccl_init_fail: every rank's communicator "fails" to come up)
+  const bool want_rccl = dcfg_.algo != 2 && (!dup_gpu || mock_rccl_fail_);
   if (want_rccl) {
-    std::string id(sizeof(ncclUniqueId), '\0');
-    if (rank_ == 0) id = device::DevicePlane::NewUniqueId();
+    // the id travels with a validity byte: a rank 0 that cannot create one tells everyone
+    std::string id(sizeof(ncclUniqueId) + 1, '\0');
+    if (rank_ == 0) {
+      try {
+        id = device::DevicePlane::NewUniqueId() + '\1';
+      } catch (const std::exception &e) {
+        utils::HandleLogInfo("[xrabit] RCCL unavailable: %s\n", e.what());
+      }
+    }
     s = host_->TreeBroadcast(&id[0], id.size(), 0);
     if (s != Status::kSuccess) return s;
-    s = dev_->InitComm(id, n, rank_, MakeProbe());
+    int rccl_ok = 0;
+    if (id.back() == '\1' && !mock_rccl_fail_) {
+      id.pop_back();
+      rccl_ok = dev_->InitComm(id, n, rank_, MakeProbe()) == Status::kSuccess ? 1 : 0;
+    }
+    // a communicator that did not come up on every rank is an environment problem, not a peer
+    // failure (retrying would fail the same way): every rank drops RCCL and the job runs on the
+    // direct transport when it has one
+    s = host_->Allreduce(&rccl_ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
     if (s != Status::kSuccess) return s;
+    if (!rccl_ok) {
+      dev_->DropComm();
+      rccl_failed_ += 1;
+      utils::HandleLogInfo("[%d] RCCL communicator did not come up on every rank: %s\n", rank_,
+                           dev_->has_peers() ? "running on the direct transport alone"
+                                             : "no device transport left");
+    }
   }
   utils::Check(dev_->ready(),
                "no device transport: ranks share a GPU (RCCL refuses) and the direct IPC "
@@ -951,6 +975,7 @@ std::string EngineBase::StatsJson() const {
      << calib_form_us_[2] << "," << calib_form_us_[3] << "]"
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
+     << ",\"rccl_init_failed\":" << rccl_failed_
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)
      << ",\"peer_links\":" << (dev_ ? dev_->PeerLinksJson() : std::string("[]"));

@@ -246,6 +246,8 @@ class EngineBase : public IEngine {
   static constexpr int kCalibForms = 4;
   double calib_form_us_[kCalibForms]{-1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
+  bool mock_rccl_fail_{false};  // test hook: the RCCL communicator never comes up
+  int rccl_failed_{0};          // epochs whose RCCL communicator did not come up on every rank
   bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
   double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long
   double dev_wait_limit_sec_{600};  // watchdog: a wait on this rank's GPU may last this long

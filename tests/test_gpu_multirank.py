@@ -212,3 +212,15 @@ def test_forced_rccl_on_shared_gpu_fails_fast():
     assert rc != 0
     assert "no device transport" in out and "rabit_device_algo=rccl" in out, out[-3000:]
     assert time.time() - t0 < 90
+
+
+def test_rccl_init_failure_falls_back_to_direct():
+    """a communicator that does not come up on every rank (rabit_mock_rccl_init_fail) is an
+    environment problem, not a peer failure: every rank agrees to drop RCCL and the job runs on
+    the direct transport instead of looping through recovery"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_multi.py", 2, ["rabit_mock_rccl_init_fail=1"], attempts=1, timeout=180)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVMULTI OK") == 2, out[-3000:]
+    assert "running on the direct transport alone" in out, out[-3000:]
