@@ -3,13 +3,18 @@ vs a raw ctypes call vs the GPU work alone (async, so the loop rate is the host 
 host is slower than the GPU)."""
 import ctypes
 import json
+import sys
 import time
 
 import torch
 
 import rabit_amd as rabit
 
-rabit.init([], lib="standard", rabit_world1_fastpath=0)
+if "--torchrun" in sys.argv:  # as bench.py starts it: tracker in-process, world 1
+    from rabit_amd.torchrun import init_from_env
+    init_from_env(lib="standard", rabit_world1_fastpath=0, rabit_device=0)
+else:
+    rabit.init([], lib="standard", rabit_world1_fastpath=0)
 L = rabit.lib()
 dev = torch.device("cuda", 0)
 res = {}
@@ -23,6 +28,7 @@ for n in (256, 32 << 20):
     t0 = time.perf_counter()
     for _ in range(N):
         rabit.allreduce(x, rabit.SUM)
+    res["py_wrapper_issue_us_n%d" % n] = (time.perf_counter() - t0) / N * 1e6
     torch.cuda.synchronize()
     res["py_wrapper_us_n%d" % n] = (time.perf_counter() - t0) / N * 1e6
     ptr = ctypes.c_void_p(x.data_ptr())
