@@ -12,7 +12,10 @@
  *  - hand-off (MI355X_MICROARCH.md, "inter-workgroup visibility"): every handed-off byte is in
  *    the uncached stage allocations, so the producer only waits for its stores to complete
  *    (s_waitcnt vmcnt(0) in every wave, workgroup barrier) before wave 0 stores the epoch into
- *    the flags (relaxed, system scope: no L2 write-back of unrelated dirty lines per tile).
+ *    the flags (relaxed, system scope).  Bytes it pushes into a peer's stage go through this
+ *    GPU's mapping of that memory, which may be cacheable here: they leave as system-scope
+ *    write-through stores (sc0 sc1), and a tile with element-wise tails releases at system scope
+ *    (L2 write-back) before its flag.
  *    Consumer: wave 0 polls (relaxed, s_sleep back-off), one system-scope acquire fence (a peer's
  *    mapping may be cacheable on this GPU), vmcnt(0), workgroup barrier, then loads;
  *  - every poll gives up on the host abort word (peer failure seen on the TCP control plane), the
@@ -41,6 +44,8 @@ using namespace vec;  // NOLINT
 
 constexpr int kBlock = 256;
 constexpr int kFlagBase = 64;  // u64 words before the ready array (word 0: mailbox)
+constexpr int kCpolSystem = 1 | 16;      // cache policy sc0 | sc1: system scope, write-through
+constexpr int kRsrcWord3 = 0x00020000;   // buffer descriptor word 3 for raw 32-bit offsets (gfx950)
 
 __device__ __forceinline__ unsigned long long *ReadyFlag(const FusedAllreduceArgs &a, int owner,
                                                          int i) {
@@ -80,10 +85,19 @@ __device__ __forceinline__ void TileRange(const FusedAllreduceArgs &a, int q, in
  *        write-back is needed (the out / out2 results are only read after the launch).
  */
 template <typename FlagOf>
-__device__ __forceinline__ void Publish(const FusedAllreduceArgs &a, int nflags, FlagOf flag) {
+__device__ __forceinline__ void Publish(const FusedAllreduceArgs &a, int nflags, FlagOf flag,
+                                        bool remote_stores = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64) {
+    if (remote_stores) {
+      // some handed-off bytes went into a PEER's memory with plain stores (element-wise tails):
+      // this GPU's mapping of it may be cacheable, so write this XCD's L2 back (system-scope
+      // release) before the flag; the wait keeps the flag behind the write-back
+      // (MI355X_MICROARCH.md, compiler hazard)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int k = static_cast<int>(threadIdx.x);
     if (k < nflags) {
       unsigned long long *f = flag(k);
@@ -129,10 +143,27 @@ __device__ __forceinline__ bool Await(const FusedAllreduceArgs &a, int *s_bad, i
   return *s_bad == 0;
 }
 
+/*! \brief 16-byte store of v at byte offset `off` of the buffer `rs` describes.  REMOTE: a peer's
+ *  memory through this GPU's mapping of it, which may be cacheable here, so the store is
+ *  system-scope write-through (cache policy sc0 sc1): once it completes (vmcnt) it is visible to
+ *  the peer with no L2 write-back of this XCD (MI355X_MICROARCH.md, inter-workgroup visibility;
+ *  cdna_hip_programming.md Guideline 16 R1, at system instead of agent scope) */
+template <bool REMOTE>
+__device__ __forceinline__ void StoreStage(uint4 *dv, __amdgpu_buffer_rsrc_t rs, size_t v, uint4 x) {
+  if (REMOTE) {
+    u32x4_t w = {x.x, x.y, x.z, x.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(v * 16), 0, kCpolSystem);
+  } else {
+    dv[v] = x;
+  }
+}
+
 /*! \brief d[0, n) = prep(s[0, n)) by the workgroup: 4 x 16-byte loads in flight per lane when
- *  both are 16-byte aligned (d always is: stage memory), element-wise otherwise */
-template <typename T>
-__device__ __forceinline__ void CopyPrep(T *d, const T *s, size_t n, int prep, T alpha,
+ *  both are 16-byte aligned (d always is: stage memory), element-wise otherwise.  Returns true
+ *  if any element went out element-wise (plain stores: a REMOTE hand-off of those needs a
+ *  system-scope release before its flag). */
+template <typename T, bool REMOTE>
+__device__ __forceinline__ bool CopyPrep(T *d, const T *s, size_t n, int prep, T alpha,
                                          bool vec_src) {
   constexpr size_t L = 16 / sizeof(T);
   size_t nvec = 0;
@@ -140,6 +171,10 @@ __device__ __forceinline__ void CopyPrep(T *d, const T *s, size_t n, int prep, T
     nvec = n / L;
     const uint4 *sv = reinterpret_cast<const uint4 *>(s);
     uint4 *dv = reinterpret_cast<uint4 *>(d);
+    // one descriptor per call (d and n are uniform over the workgroup; n * sizeof(T) is at most
+    // one tile, far below the 4 GiB of a descriptor's 32-bit offsets)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(d, 0, static_cast<int>(nvec * 16), kRsrcWord3);
     size_t v = threadIdx.x;
     for (; v + 3 * kBlock < nvec; v += 4 * kBlock) {
       uint4 t[4];
@@ -150,13 +185,14 @@ __device__ __forceinline__ void CopyPrep(T *d, const T *s, size_t n, int prep, T
         for (int u = 0; u < 4; ++u) t[u] = PrepVec<T>(t[u], prep, alpha);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) dv[v + u * kBlock] = t[u];
+      for (int u = 0; u < 4; ++u) StoreStage<REMOTE>(dv, rs, v + u * kBlock, t[u]);
     }
     for (; v < nvec; v += kBlock) {
-      dv[v] = prep == kPrepCopy ? sv[v] : PrepVec<T>(sv[v], prep, alpha);
+      StoreStage<REMOTE>(dv, rs, v, prep == kPrepCopy ? sv[v] : PrepVec<T>(sv[v], prep, alpha));
     }
   }
   for (size_t e = nvec * L + threadIdx.x; e < n; e += kBlock) d[e] = PrepApply<T>(s[e], prep, alpha);
+  return nvec * L < n;
 }
 
 /*! \brief store the 16-byte vector v as elements [e, e + 16 / sizeof(T)) of dst */
@@ -195,19 +231,27 @@ __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduce
 
   // ---- 1. stage (pull) or push this workgroup's tiles of every segment, then publish them
   for (int i = blockIdx.x; i < a.tiles; i += gridDim.x) {
+    bool scalar_remote = false;  // some pushed element left with a plain (cacheable) store
     if (a.push || !a.zero_copy) {
       for (int q = 0; q < n; ++q) {
         size_t lo, hi;
         TileRange(a, q, i, &lo, &hi);
         if (hi <= lo) continue;
-        T *d = a.push ? reinterpret_cast<T *>(a.stage[q]) + static_cast<size_t>(r) * a.seg +
-                            (lo - static_cast<size_t>(q) * a.seg)
-                      : mine + lo;
-        CopyPrep<T>(d, src + lo, hi - lo, a.prep, alpha, vsrc);
+        if (a.push && q != r) {
+          T *d = reinterpret_cast<T *>(a.stage[q]) + static_cast<size_t>(r) * a.seg +
+                 (lo - static_cast<size_t>(q) * a.seg);
+          scalar_remote |= CopyPrep<T, true>(d, src + lo, hi - lo, a.prep, alpha, vsrc);
+        } else {
+          T *d = a.push ? reinterpret_cast<T *>(a.stage[q]) + static_cast<size_t>(r) * a.seg +
+                              (lo - static_cast<size_t>(q) * a.seg)
+                        : mine + lo;
+          CopyPrep<T, false>(d, src + lo, hi - lo, a.prep, alpha, vsrc);
+        }
       }
     }
     if (a.push) {
-      Publish(a, n, [&](int q) { return InboxFlag(a, q, r, i); });
+      // scalar_remote is the same in every thread of the workgroup (sizes and alignment only)
+      Publish(a, n, [&](int q) { return InboxFlag(a, q, r, i); }, scalar_remote);
     } else {
       // pull: where this rank's input is (its stage, or its input in place in the symmetric
       // heap) goes out with the flag; every rank chooses for itself
