@@ -389,6 +389,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       // remote writes, read from the input where it is), then every inbox is local memory
       CopyBatch b;
       NewBatch(&b);
+      b.remote = 1;  // (this rank's own inbox slot too: the same store kind everywhere)
       for (int q = 0; q < n_; ++q) {
         size_t qlo, qhi;
         SegRange(c, seg, q, &qlo, &qhi);

@@ -69,6 +69,7 @@ struct CopyBatch {
   CopySeg seg[kMaxCopySegs];
   int n;
   const int *guard;  // optional device word: the launch does nothing when it is non-zero
+  int remote;        // 1: every dst is a peer's memory (push): system-scope write-through stores
 };
 
 /*!
@@ -282,6 +283,7 @@ class PeerGroup {
   void NewBatch(CopyBatch *b) const {
     b->n = 0;
     b->guard = dev_status();
+    b->remote = 0;
   }
 
   int device_;

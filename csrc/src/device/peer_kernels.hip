@@ -90,8 +90,41 @@ __device__ __forceinline__ void StoreNT(uint4 *p, uint4 v) {
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
 }
 
-__device__ __forceinline__ bool Al16(const void *p) {
+__host__ __device__ __forceinline__ bool Al16(const void *p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+/*!
+ * \brief one tile of a push segment into a peer's memory.  The destination is reached through
+ *        this GPU's mapping of the peer's allocation, which may be cacheable here, so every byte
+ *        leaves with a 16-byte system-scope write-through store (sc0 sc1): once the kernel has
+ *        ended the peer sees it, whatever its cache type (the barrier kernel that follows signals
+ *        from one workgroup, whose release cannot write back the other XCDs' L2s).  The inbox
+ *        slot is 16-byte aligned and padded to whole 256-element blocks, so a tail word may carry
+ *        zero padding past `bytes`; the source is read only within `bytes`.
+ */
+__device__ __forceinline__ void PushTile(const CopySeg &g, size_t lo, size_t hi) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const size_t nw = (hi - lo + 15) / 16;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      g.dst + lo, 0, static_cast<int>(nw * 16), 0x00020000);
+  const bool vsrc = Al16(g.src + lo);
+  for (size_t w = threadIdx.x; w < nw; w += kBlock) {
+    uint4 v;
+    if (vsrc && lo + (w + 1) * 16 <= hi) {
+      v = reinterpret_cast<const uint4 *>(g.src + lo)[w];
+    } else {
+      unsigned char b[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const size_t at = lo + w * 16 + k;
+        b[k] = at < hi ? static_cast<unsigned char>(g.src[at]) : 0;
+      }
+      __builtin_memcpy(&v, b, 16);
+    }
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, static_cast<int>(w * 16), 0, 1 | 16);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
@@ -105,6 +138,10 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
   const size_t lo = tile * kTileBytes;
   if (lo >= g.bytes) return;
   const size_t hi = std::min(g.bytes, lo + kTileBytes);
+  if (batch.remote) {
+    PushTile(g, lo, hi);
+    return;
+  }
   const bool vec = Al16(g.dst) && Al16(g.src) && (g.dst2 == nullptr || Al16(g.dst2));
   if (vec) {
     const size_t nv = (hi - lo) / 16;  // lo is a multiple of 16
@@ -162,6 +199,10 @@ hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsign
 
 hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream) {
   if (batch.n < 0 || batch.n > kMaxCopySegs) return hipErrorInvalidValue;
+  for (int i = 0; i < batch.n && batch.remote; ++i) {
+    // push destinations are whole-16-byte inbox slots (PushTile pads the last word)
+    if (!Al16(batch.seg[i].dst) || batch.seg[i].dst2 != nullptr) return hipErrorInvalidValue;
+  }
   size_t tiles = 0;
   for (int i = 0; i < batch.n; ++i) {
     tiles = std::max(tiles, (batch.seg[i].bytes + kTileBytes - 1) / kTileBytes);
