@@ -260,6 +260,9 @@ def main():
                     help="after the timed loop, also time the other BASELINE configs: 1 GiB "
                          "broadcast, 64 MiB lazy (squared-gradient) allreduce fused vs unfused, "
                          "256 MiB HBM checkpoint")
+    ap.add_argument("--rccl-tune", type=int, default=1,
+                    help="N > 1: time RCCL's own channel count against fixed CTA counts at "
+                         "start-up and keep the fastest")
     ap.add_argument("--deadline", type=int, default=900,
                     help="wall-clock limit of the whole run in seconds")
     args = ap.parse_args()
@@ -289,8 +292,11 @@ def main():
     heap_bytes = n * 4 + (48 << 20) if (world > 1 and args.variants) or args.symmetric else 0
     heap = {"rabit_device_symmetric_heap": str(heap_bytes)} if heap_bytes else {}
     phase("init")
+    # N > 1: RCCL's channel (CTA) count is timed at start-up against fixed counts and the
+    # fastest communicator is kept (transport.rccl_tuning)
+    tune = {"rabit_rccl_tune": "1"} if world > 1 and args.rccl_tune else {}
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
-                        rabit_world1_fastpath=0, rabit_device=gpu, **heap)
+                        rabit_world1_fastpath=0, rabit_device=gpu, **heap, **tune)
     dev = torch.device("cuda", gpu)
 
     phase("reference")
@@ -385,7 +391,8 @@ def main():
                       "direct_fused": bool(st.get("direct_fused", 0)),
                       "fused_chunks": st.get("fused_chunks", 0),
                       "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),
-                      "peer_links": st.get("peer_links")},
+                      "peer_links": st.get("peer_links"),
+                      "rccl_tuning": st.get("rccl_tuning")},
         "variants": variants,
         "extras": extras,
         "reference_measured": reference_measured(world, aggregate),

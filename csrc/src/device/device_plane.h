@@ -207,6 +207,12 @@ class DevicePlane {
   size_t direct_min_bytes() const { return cfg_.direct_min_bytes; }
   /*! \brief calibration: -1 normal routing, 0 force RCCL, 1 force direct */
   void ForceTransport(int which) { force_ = which; }
+  /*! \brief channel (CTA) bounds of the next communicator (0: RCCL's choice) */
+  void set_rccl_ctas(int min_ctas, int max_ctas) {
+    cfg_.rccl_min_ctas = min_ctas;
+    cfg_.rccl_max_ctas = max_ctas;
+  }
+  int rccl_min_ctas() const { return cfg_.rccl_min_ctas; }
   /*! \brief direct reduce-scatter by remote writes (push) instead of remote reads */
   void SetDirectPush(bool v) {
     if (peers_ != nullptr) peers_->set_push(v);

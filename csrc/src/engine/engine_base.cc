@@ -106,6 +106,8 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
   if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
+  if (is("rabit_rccl_tune")) rccl_tune_ = utils::StringToBool(val);
+  if (is("rabit_rccl_tune_ctas")) rccl_tune_ctas_ = val;
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
     if (!strcmp(val, "auto")) {
@@ -390,40 +392,34 @@ Status EngineBase::EnsureDeviceComm() {
   // (test hook rabit_mock_rccl_init_fail: every rank's communicator "fails" to come up)
   const bool want_rccl = dcfg_.algo != 2 && (!dup_gpu || mock_rccl_fail_);
   if (want_rccl) {
-    // the id travels with a validity byte: a rank 0 that cannot create one tells everyone
-    std::string id(sizeof(ncclUniqueId) + 1, '\0');
-    if (rank_ == 0) {
-      try {
-        id = device::DevicePlane::NewUniqueId() + '\1';
-      } catch (const std::exception &e) {
-        utils::HandleLogInfo("[xrabit] RCCL unavailable: %s\n", e.what());
-      }
-    }
-    s = host_->TreeBroadcast(&id[0], id.size(), 0);
+    bool up = false;
+    s = BuildRccl(&up);
     if (s != Status::kSuccess) return s;
-    int rccl_ok = 0;
-    if (id.back() == '\1' && !mock_rccl_fail_) {
-      id.pop_back();
-      rccl_ok = dev_->InitComm(id, n, rank_, MakeProbe()) == Status::kSuccess ? 1 : 0;
-    }
-    // a communicator that did not come up on every rank is an environment problem, not a peer
-    // failure (retrying would fail the same way): every rank drops RCCL and the job runs on the
-    // direct transport when it has one
-    s = host_->Allreduce(&rccl_ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
-    if (s != Status::kSuccess) return s;
-    if (!rccl_ok) {
-      dev_->DropComm();
+    if (!up) {
       rccl_failed_ += 1;
       utils::HandleLogInfo("[%d] RCCL communicator did not come up on every rank: %s\n", rank_,
                            dev_->has_peers() ? "running on the direct transport alone"
                                              : "no device transport left");
     }
   }
-  utils::Check(dev_->ready(),
-               "no device transport: ranks share a GPU (RCCL refuses) and the direct IPC "
-               "transport is %s",
+  utils::Check(dev_->ready(), "no device transport: %s and the direct IPC transport is %s",
+               dup_gpu ? "ranks share a GPU (RCCL refuses)"
+                       : (dcfg_.algo == 2 ? "RCCL is disabled (rabit_device_algo=direct)"
+                                          : "the RCCL communicator did not come up"),
                dcfg_.algo == 1 ? "disabled (rabit_device_algo=rccl)" : "unavailable");
   dev_->BeginEpoch(n, rank_);
+  if (want_rccl) {
+    // every rank takes part in a tuning or none does (a restarted rank adopts the survivors'
+    // choice through BuildRccl's agreement on the CTA bounds)
+    int tune = rccl_tune_ && !rccl_tuned_ && dev_->has_comm() ? 1 : 0;
+    s = host_->Allreduce(&tune, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+    if (s != Status::kSuccess) return s;
+    rccl_tuned_ = true;
+    if (tune) {
+      s = TuneRcclChannels();
+      if (s != Status::kSuccess) return s;
+    }
+  }
   if ((dev_->has_comm() || calibrate_test_) && dev_->has_peers() && dcfg_.algo == 0 &&
       calibrate_) {
     s = CalibrateDevice();
@@ -434,6 +430,119 @@ Status EngineBase::EnsureDeviceComm() {
                          rank_, dev_->epoch(), dev_->has_comm() ? 1 : 0,
                          dev_->has_peers() ? 1 : 0, dcfg_.direct_min_bytes);
   }
+  return Status::kSuccess;
+}
+
+Status EngineBase::BuildRccl(bool *up) {
+  *up = false;
+  // the CTA bounds of the communicator: the largest any rank holds (a restarted rank has none
+  // yet and adopts the survivors' tuned value), so every rank asks RCCL for the same
+  int ctas[2] = {dev_->rccl_min_ctas(), dev_->config().rccl_max_ctas};
+  Status s = host_->Allreduce(ctas, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMax));
+  if (s != Status::kSuccess) return s;
+  dev_->set_rccl_ctas(ctas[0], ctas[1]);
+  // the id travels with a validity byte: a rank 0 that cannot create one tells everyone
+  std::string id(sizeof(ncclUniqueId) + 1, '\0');
+  if (rank_ == 0) {
+    try {
+      id = device::DevicePlane::NewUniqueId() + '\1';
+    } catch (const std::exception &e) {
+      utils::HandleLogInfo("[xrabit] RCCL unavailable: %s\n", e.what());
+    }
+  }
+  s = host_->TreeBroadcast(&id[0], id.size(), 0);
+  if (s != Status::kSuccess) return s;
+  int ok = 0;
+  if (id.back() == '\1' && !mock_rccl_fail_) {
+    id.pop_back();
+    ok = dev_->InitComm(id, GetWorldSize(), rank_, MakeProbe()) == Status::kSuccess ? 1 : 0;
+  }
+  // a communicator that did not come up on every rank is an environment problem, not a peer
+  // failure (retrying would fail the same way): every rank drops it
+  s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  if (!ok) dev_->DropComm();
+  *up = ok != 0;
+  return Status::kSuccess;
+}
+
+Status EngineBase::TuneRcclChannels() {
+  // one 128 MiB float32 sum per repetition, both destinations (as the robust engine runs it),
+  // best of 3 after a warm-up, max over ranks; the candidates are RCCL's own channel choice and
+  // fixed CTA counts (one CTA drives one channel: more channels, more of the 7 links busy)
+  const size_t count = std::max<size_t>(dcfg_.calib_big / 4, 1u << 20);
+  float *src = static_cast<float *>(dev_->Scratch(count * 4, 0));
+  float *dst = static_cast<float *>(dev_->Scratch(count * 4, 1));
+  float *dst2 = static_cast<float *>(dev_->Scratch(count * 4, device::DevicePlane::kCalibScratch));
+  device::CheckHip(device::LaunchFill(src, count, mpi::kFloat, 1.0, dev_->stream()), "LaunchFill");
+  std::vector<int> cands = {0};
+  {
+    std::istringstream in(rccl_tune_ctas_);
+    std::string c;
+    while (std::getline(in, c, ',')) {
+      if (atoi(c.c_str()) > 0) cands.push_back(atoi(c.c_str()));
+    }
+  }
+  const int base_min = dev_->rccl_min_ctas(), base_max = dev_->config().rccl_max_ctas;
+  std::vector<double> times(cands.size(), 1e30);
+  for (size_t i = 0; i < cands.size(); ++i) {
+    if (i > 0) {
+      dev_->DropComm();
+      dev_->set_rccl_ctas(cands[i], cands[i]);
+      bool up = false;
+      Status s = BuildRccl(&up);
+      if (s != Status::kSuccess) return s;
+      if (!up) continue;  // this bound refused on some rank: skip it
+    }
+    dev_->ForceTransport(0);
+    double best = 1e30;
+    for (int rep = 0; rep < 4; ++rep) {
+      const double t0 = utils::GetTime();
+      Status s = dev_->Allreduce(src, dst, dst2, count, mpi::kFloat, mpi::kSum, device::kPrepCopy,
+                                 1.0, MakeProbe());
+      if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+      if (s != Status::kSuccess) {
+        dev_->ForceTransport(-1);
+        return s;  // a failed RCCL op: a real failure, the caller recovers
+      }
+      dev_->Synchronize();
+      if (rep > 0) best = std::min(best, utils::GetTime() - t0);
+    }
+    dev_->ForceTransport(-1);
+    times[i] = best;
+  }
+  Status s = host_->Allreduce(times.data(), sizeof(double), times.size(),
+                              coll::HostReducer(mpi::kDouble, mpi::kMax));
+  if (s != Status::kSuccess) return s;
+  size_t best = 0;
+  for (size_t i = 1; i < cands.size(); ++i) {
+    if (times[i] < times[best]) best = i;
+  }
+  std::ostringstream js;
+  js << "{\"bytes\":" << count * 4 << ",\"us\":{";
+  for (size_t i = 0; i < cands.size(); ++i) {
+    js << (i ? "," : "") << "\"" << (cands[i] ? std::to_string(cands[i]) : "rccl") << "\":"
+       << (times[i] < 1e29 ? times[i] * 1e6 : -1.0);
+  }
+  js << "},\"chosen\":\"" << (cands[best] ? std::to_string(cands[best]) : "rccl") << "\"}";
+  rccl_tune_json_ = js.str();
+  if (rank_ == 0 || debug_) {
+    utils::HandleLogInfo("[xrabit] RCCL channel tuning: %s\n", rccl_tune_json_.c_str());
+  }
+  // the communicator in place is the last candidate's; rebuild with the winner if it differs
+  const int want_min = cands[best] ? cands[best] : base_min;
+  const int want_max = cands[best] ? cands[best] : base_max;
+  if (best != cands.size() - 1 || times[best] >= 1e29) {
+    dev_->DropComm();
+    dev_->set_rccl_ctas(want_min, want_max);
+    bool up = false;
+    s = BuildRccl(&up);
+    if (s != Status::kSuccess) return s;
+    if (!up) rccl_failed_ += 1;
+  }
+  // later epochs (after a recovery) build with the same bounds
+  dcfg_.rccl_min_ctas = want_min;
+  dcfg_.rccl_max_ctas = want_max;
   return Status::kSuccess;
 }
 
@@ -976,6 +1085,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"rccl_init_failed\":" << rccl_failed_
+     << ",\"rccl_tuning\":" << rccl_tune_json_
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)
      << ",\"peer_links\":" << (dev_ ? dev_->PeerLinksJson() : std::string("[]"));

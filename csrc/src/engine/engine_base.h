@@ -166,6 +166,12 @@ class EngineBase : public IEngine {
   /*! \brief auto mode: time RCCL and the direct transport at two sizes, verify the direct
    *  result, and set the size from which ops go direct (collective) */
   Status CalibrateDevice();
+  /*! \brief collective: time the 128 MiB RCCL allreduce with RCCL's own channel count and
+   *  with fixed CTA counts (rabit_rccl_tune_ctas), keep the fastest communicator */
+  Status TuneRcclChannels();
+  /*! \brief collective: (re)build the RCCL communicator of this epoch with the current CTA
+   *  bounds; false on every rank if it did not come up on every rank */
+  Status BuildRccl(bool *up);
   /*! \brief (re)connect peer links through the tracker */
   bool ReconnectLinks(const char *cmd);
   /*! \brief true if any peer link hung up (used while waiting on device ops) */
@@ -247,7 +253,11 @@ class EngineBase : public IEngine {
   double calib_form_us_[kCalibForms]{-1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
   bool mock_rccl_fail_{false};  // test hook: the RCCL communicator never comes up
-  int rccl_failed_{0};          // epochs whose RCCL communicator did not come up on every rank
+  int rccl_failed_{0};
+  bool rccl_tune_{false};          // rabit_rccl_tune: time RCCL channel counts at start-up
+  bool rccl_tuned_{false};         // this process took part in (or adopted) a tuning
+  std::string rccl_tune_ctas_{"64,112"};  // candidate CTA counts besides RCCL's own choice
+  std::string rccl_tune_json_{"{}"};      // what the tuning measured (stats)          // epochs whose RCCL communicator did not come up on every rank
   bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
   double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long
   double dev_wait_limit_sec_{600};  // watchdog: a wait on this rank's GPU may last this long

@@ -53,6 +53,13 @@ st = rabit.stats()
 want_rccl = algo in ("rccl", "auto")
 assert st["device_rccl"] == (1 if want_rccl else 0), st
 assert st["device_direct"] == (1 if algo in ("direct", "auto") else 0), st
+tuning = st.get("rccl_tuning", {})
+if any(a.startswith("rabit_rccl_tune=1") for a in sys.argv[2:]) and want_rccl:
+    # the channel tuning timed RCCL's own choice and every candidate, kept one communicator
+    assert set(tuning.get("us", {})) == {"rccl", "4", "16"}, tuning
+    assert all(t > 0 for t in tuning["us"].values()), tuning
+    assert tuning["chosen"] in tuning["us"], tuning
 rabit.checkpoint(None)
 rabit.finalize()
-print("TRANSPORT1 OK algo=%s cases=%d calib=%s" % (algo, checked, st.get("calib_us")), flush=True)
+print("TRANSPORT1 OK algo=%s cases=%d calib=%s tuning=%s" % (algo, checked, st.get("calib_us"),
+                                                             tuning), flush=True)

@@ -116,13 +116,14 @@ def test_bench_n1(tmp_path):
     assert rec["n_gpus"] == 1 and rec["value"] > 0
 
 
-@pytest.mark.parametrize("algo", ["rccl", "direct", "auto"])
-def test_transports_world1(algo):
+@pytest.mark.parametrize("algo,extra", [("rccl", []), ("direct", []), ("auto", []),
+                                        ("auto", ["rabit_rccl_tune=1", "rabit_rccl_tune_ctas=4,16"])])
+def test_transports_world1(algo, extra):
     """RCCL and direct-transport API paths on the box's one GPU (a one-rank communicator /
     group): the 8-GPU runs use the same calls with more ranks."""
     from rabit_amd.launcher import LocalJob
     job = LocalJob([sys.executable, os.path.join(ROOT, "tests", "scripts", "transport_world1.py"),
-                    algo], 1, 1, capture=True, timeout=240, print_fn=lambda m: None)
+                    algo] + extra, 1, 1, capture=True, timeout=240, print_fn=lambda m: None)
     rc = job.run()
     out = "".join("".join(o) for o in job.outputs)
     assert rc == 0, out[-5000:]
