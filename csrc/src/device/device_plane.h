@@ -201,9 +201,14 @@ class DevicePlane {
   bool UseDirect(size_t bytes) const {
     if (peers_ == nullptr) return false;
     if (force_ >= 0) return force_ == 1;
-    return comm_ == nullptr || cfg_.algo == 2 || bytes >= cfg_.direct_min_bytes;
+    return comm_ == nullptr || cfg_.algo == 2 || bytes >= cfg_.direct_min_bytes ||
+           bytes < direct_below_bytes_;
   }
   void set_direct_min_bytes(size_t b) { cfg_.direct_min_bytes = b; }
+  /*! \brief ops below this size go direct too (the calibration found the direct transport
+   *  faster for small ops and RCCL for large ones) */
+  void set_direct_below_bytes(size_t b) { direct_below_bytes_ = b; }
+  size_t direct_below_bytes() const { return direct_below_bytes_; }
   size_t direct_min_bytes() const { return cfg_.direct_min_bytes; }
   /*! \brief calibration: -1 normal routing, 0 force RCCL, 1 force direct */
   void ForceTransport(int which) { force_ = which; }
@@ -329,6 +334,7 @@ class DevicePlane {
   SymHeapInfo heap_;
   size_t heap_used_{0};
   int force_{-1};
+  size_t direct_below_bytes_{0};
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};
   size_t pending_bytes_{0};

@@ -700,11 +700,18 @@ Status EngineBase::CalibrateDevice() {
     const double x0 = sizes[0] * 4.0, x1 = sizes[1] * 4.0;
     const double br = (agg[1] - agg[0]) / (x1 - x0), bd = (agg[3] - agg[2]) / (x1 - x0);
     const double ar = agg[0] - br * x0, ad = agg[2] - bd * x0;
+    size_t below = 0;
     if (agg[3] < agg[1]) {
       const double cross = bd < br ? (ad - ar) / (br - bd) : 0.0;
       threshold = static_cast<size_t>(std::max(0.0, std::min(cross, x1)));
+    } else if (agg[2] < agg[0]) {
+      // direct faster at the small point, RCCL at the large one: direct below the crossover
+      // (the latency path: one barrier and one-shot reads against RCCL's launch and protocol)
+      const double cross = bd > br ? (ar - ad) / (bd - br) : x1;
+      below = static_cast<size_t>(std::max(x0, std::min(cross, x1)));
     }
     dev_->set_direct_min_bytes(threshold);
+    dev_->set_direct_below_bytes(below);
   }
   calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
             static_cast<double>(sizes[1] * 4), agg[4 + 2] > 0 ? agg[4 + 2] : 0.0};
@@ -718,8 +725,11 @@ Status EngineBase::CalibrateDevice() {
         dev_->direct_push() ? "push" : "pull", forms[best].fused ? "fused" : "classic",
         calib_form_us_[0], calib_form_us_[1], calib_form_us_[2], calib_form_us_[3],
         !ok ? "disabled (failed verification)"
-            : (threshold == static_cast<size_t>(-1) ? "off (RCCL faster)"
-                                                    : ("from " + std::to_string(threshold) + " B").c_str()));
+            : (threshold != static_cast<size_t>(-1)
+                   ? ("from " + std::to_string(threshold) + " B").c_str()
+                   : (dev_->direct_below_bytes() > 0
+                          ? ("below " + std::to_string(dev_->direct_below_bytes()) + " B").c_str()
+                          : "off (RCCL faster)")));
   }
   return Status::kSuccess;
 }
@@ -1077,6 +1087,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"symmetric_heap_used\":" << (dev_ ? dev_->sym_heap_used() : 0)
      << ",\"device_direct_min\":"
      << (dev_ && dev_->has_peers() ? static_cast<double>(dev_->direct_min_bytes()) : -1.0)
+     << ",\"device_direct_below\":" << (dev_ ? dev_->direct_below_bytes() : 0)
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
      << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
      << ",\"calib_push_us\":" << calib_.push_big * 1e6

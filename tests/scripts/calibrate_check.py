@@ -22,6 +22,13 @@ thr = st["device_direct_min"]
 lo = rabit.allreduce(np.array([thr]), rabit.MIN)[0]
 hi = rabit.allreduce(np.array([thr]), rabit.MAX)[0]
 assert lo == hi, (lo, hi)
+# the small-op window (direct below a crossover when RCCL wins at the large point) is uniform too,
+# and never overlaps the large-op threshold
+below = st["device_direct_below"]
+blo = rabit.allreduce(np.array([below]), rabit.MIN)[0]
+bhi = rabit.allreduce(np.array([below]), rabit.MAX)[0]
+assert blo == bhi, (blo, bhi)
+assert below == 0 or thr >= 2 ** 63, (below, thr)
 # the push variant was timed and the pull/push choice is the same everywhere
 assert st["calib_push_us"] > 0, st
 push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
