@@ -382,6 +382,7 @@ def main():
         "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),
                       "zero_copy_chunks": st.get("zero_copy_chunks", 0),
                       "direct_min_bytes": st.get("device_direct_min", -1),
+                      "direct_below_bytes": st.get("device_direct_below", 0),
                       "calibration_us": st.get("calib_us"),
                       "direct_variant": "push" if st.get("direct_push") else "pull",
                       "calibration_push_us": st.get("calib_push_us"),
