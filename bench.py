@@ -263,7 +263,7 @@ def main():
     ap.add_argument("--rccl-tune", type=int, default=1,
                     help="N > 1: time RCCL's own channel count against fixed CTA counts at "
                          "start-up and keep the fastest")
-    ap.add_argument("--deadline", type=int, default=900,
+    ap.add_argument("--deadline", type=int, default=600,
                     help="wall-clock limit of the whole run in seconds")
     args = ap.parse_args()
 
