@@ -12,6 +12,7 @@
 
 #include "device/kernels.h"
 #include "engine/engine_base.h"
+#include "engine/routing.h"
 #include "rabit/internal/timer.h"
 #include "rabit/internal/utils.h"
 
@@ -370,23 +371,12 @@ Status EngineBase::CalibrateDevice() {
     dev_->SetDirectPush(forms[best].push);
     dev_->SetFused(forms[best].fused);
     agg[3] = agg[4 + best];
-    // linear model t = a + b * bytes per transport through the two points; direct from the
-    // crossover on (when its slope is smaller)
-    const double x0 = sizes[0] * 4.0, x1 = sizes[1] * 4.0;
-    const double br = (agg[1] - agg[0]) / (x1 - x0), bd = (agg[3] - agg[2]) / (x1 - x0);
-    const double ar = agg[0] - br * x0, ad = agg[2] - bd * x0;
-    size_t below = 0;
-    if (agg[3] < agg[1]) {
-      const double cross = bd < br ? (ad - ar) / (br - bd) : 0.0;
-      threshold = static_cast<size_t>(std::max(0.0, std::min(cross, x1)));
-    } else if (agg[2] < agg[0]) {
-      // direct faster at the small point, RCCL at the large one: direct below the crossover
-      // (the latency path: one barrier and one-shot reads against RCCL's launch and protocol)
-      const double cross = bd > br ? (ar - ad) / (bd - br) : x1;
-      below = static_cast<size_t>(std::max(x0, std::min(cross, x1)));
-    }
+    // linear model t = a + b * bytes per transport through the two points (routing.h)
+    const DirectRouting route =
+        ChooseDirectRouting(sizes[0] * 4.0, sizes[1] * 4.0, agg[0], agg[1], agg[2], agg[3]);
+    threshold = route.min_bytes;
     dev_->set_direct_min_bytes(threshold);
-    dev_->set_direct_below_bytes(below);
+    dev_->set_direct_below_bytes(route.below_bytes);
   }
   calib_ = {agg[0], agg[1], agg[2], agg[3], static_cast<double>(sizes[0] * 4),
             static_cast<double>(sizes[1] * 4), agg[4 + 2] > 0 ? agg[4 + 2] : 0.0};

@@ -12,6 +12,7 @@
 #include <rabit/rabit.h>
 
 #include <atomic>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <functional>
@@ -27,6 +28,7 @@
 #include "net/link_reset.h"
 #include "engine/engine_mock.h"
 #include "engine/engine_robust.h"
+#include "engine/routing.h"
 
 namespace {
 struct TestCase {
@@ -358,6 +360,32 @@ TEST(half_types_roundtrip_and_rounding) {
   EXPECT(rabit::coll::HostReducer(rabit::engine::mpi::kHalf, rabit::engine::mpi::kBitwiseOR) ==
          nullptr);
   EXPECT(rabit::coll::DTypeSize(rabit::engine::mpi::kHalf) == 2);
+}
+
+// the calibration's RCCL / direct routing (routing.h): 64 KiB and 128 MiB points, times in s
+TEST(calibration_routing) {
+  using rabit::engine::ChooseDirectRouting;
+  const double x0 = 65536, x1 = 134217728, none = static_cast<double>(static_cast<size_t>(-1));
+  // direct faster at both points with a flatter slope: direct for every size
+  auto r = ChooseDirectRouting(x0, x1, 30e-6, 900e-6, 20e-6, 700e-6);
+  EXPECT(r.min_bytes == 0 && r.below_bytes == 0);
+  // RCCL faster small, direct faster large: direct from the crossover, which lies in between
+  r = ChooseDirectRouting(x0, x1, 20e-6, 900e-6, 40e-6, 700e-6);
+  EXPECT(r.min_bytes > x0 && r.min_bytes < x1 && r.below_bytes == 0);
+  // the crossover of the two lines: equal predicted times there
+  const double br = (900e-6 - 20e-6) / (x1 - x0), bd = (700e-6 - 40e-6) / (x1 - x0);
+  const double m = static_cast<double>(r.min_bytes);
+  EXPECT(std::abs((20e-6 + br * (m - x0)) - (40e-6 + bd * (m - x0))) < 1e-9);
+  // direct faster small, RCCL faster large: direct below the crossover only
+  r = ChooseDirectRouting(x0, x1, 40e-6, 700e-6, 20e-6, 900e-6);
+  EXPECT(static_cast<double>(r.min_bytes) == none && r.below_bytes > x0 && r.below_bytes < x1);
+  // RCCL faster at both points: no direct range
+  r = ChooseDirectRouting(x0, x1, 20e-6, 700e-6, 40e-6, 900e-6);
+  EXPECT(static_cast<double>(r.min_bytes) == none && r.below_bytes == 0);
+  // direct faster at the large point only, but with a steeper slope (cannot happen with a
+  // straight line through both points unless it is faster at the small one too): from 0
+  r = ChooseDirectRouting(x0, x1, 20e-6, 900e-6, 10e-6, 890e-6);
+  EXPECT(r.min_bytes == 0);
 }
 
 TEST(wait_state_working_vs_waiting) {
