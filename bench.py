@@ -200,7 +200,8 @@ def time_steps(rabit, torch, x, steps):
 
 def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=False):
     """every transport this job has up, on torch-allocated and symmetric-heap inputs: time
-    and busbw of the 128 MiB float32 sum, each checked against the host fp64 reference"""
+    and busbw of the 128 MiB float32 sum, each checked against the host fp64 reference; plus
+    the per-phase times of the classic direct form (pull and push)"""
     out = []
     bufs = [("torch", torch.empty(n, dtype=torch.float32, device=dev))]
     try:
@@ -231,15 +232,35 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=Fals
                 rec["busbw_GBps"] = round(n * 4 / t / 1e9 * 2 * (world - 1) / world, 2)
                 rabit.checkpoint(None)  # bounded result log
             out.append(rec)
+    # where the time of the classic direct form goes (stage copy, barriers, reduce, gather),
+    # per phase from hipEvents, on the torch-allocated input: evidence for tuning the xGMI path
+    x = bufs[0][1]
+    phases = []
+    for mode in ("pull", "push"):
+        phase("phases %s" % mode)
+        up = rabit.set_device_transport(rabit.TRANSPORT_DIRECT, mode, False)
+        up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
+        if not up:
+            continue
+        rabit.set_phase_timing(True)
+        for _ in range(5):
+            rabit.allreduce(x, rabit.SUM)
+        torch.cuda.synchronize()
+        st = rabit.stats()
+        rabit.set_phase_timing(False)
+        phases.append({"transport": "direct-%s-classic" % mode, "input": "torch",
+                       "phase_us": st.get("direct_phase_us"),
+                       "timed_ops": st.get("direct_timed_ops")})
+        rabit.checkpoint(None)
     # back to the calibrated choice of transport and direct form (or to RCCL after a fallback)
     if forced_rccl:
         rabit.set_device_transport(rabit.TRANSPORT_RCCL, None)
-        return out
+        return out, phases
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
     if st0.get("device_direct"):
         rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
                                    bool(st0.get("direct_fused")))
-    return out
+    return out, phases
 
 
 def main():
@@ -336,12 +357,13 @@ def main():
     elapsed = time_steps(rabit, torch, x, args.steps)
     st_head = rabit.stats()
 
-    variants = None
+    variants = phases = None
     if world > 1 and args.variants:
         phase("variants")
         rabit.checkpoint(None)
-        variants = run_variants(rabit, torch, dev, n, world, rank, ref, max(5, args.steps // 2),
-                                forced_rccl=check_fallback is not None)
+        variants, phases = run_variants(rabit, torch, dev, n, world, rank, ref,
+                                        max(5, args.steps // 2),
+                                        forced_rccl=check_fallback is not None)
     phase("extras")
     extras = run_extras(rabit, torch, dev, world) if args.extras else {}
 
@@ -395,6 +417,7 @@ def main():
                       "peer_links": st.get("peer_links"),
                       "rccl_tuning": st.get("rccl_tuning")},
         "variants": variants,
+        "direct_phase_breakdown": phases,
         "extras": extras,
         "reference_measured": reference_measured(world, aggregate),
     }

@@ -114,6 +114,13 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode);
  * \return 0, or -1 when the direct transport is not up
  */
 RABIT_DLL int RabitDevSetFused(int fused);
+/*!
+ * \brief xrabit extension: per-phase hipEvent timing of the direct transport's classic two-shot
+ *        allreduce (stage, barrier, reduce, barrier, gather) from now on, with fresh totals
+ *        (on = 1), or off (0); averages appear in RabitGetStats as direct_phase_us.
+ * \return 0, or -1 without a direct transport
+ */
+RABIT_DLL int RabitDevSetPhaseTiming(int on);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

@@ -290,6 +290,12 @@ RABIT_DLL int RabitDevSetFused(int fused) {
   return 0;
 }
 
+RABIT_DLL int RabitDevSetPhaseTiming(int on) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) return -1;
+  return e->device_plane()->SetPhaseTiming(on != 0) ? 0 : -1;
+}
+
 RABIT_DLL const char *RabitGetLastError() { return g_last_error.c_str(); }
 
 RABIT_DLL const char *RabitGetStats() {

@@ -246,6 +246,18 @@ class DevicePlane {
     if (peers_ != nullptr) peers_->set_fused(v);
   }
   bool fused() const { return peers_ != nullptr && peers_->fused(); }
+  /*! \brief hipEvent timing of the classic direct form's phases from now on (fresh totals),
+   *  or off; false without a peer group */
+  bool SetPhaseTiming(bool on) {
+    if (peers_ == nullptr) return false;
+    if (on) {
+      peers_->EnableTiming();
+      peers_->ResetTiming();
+    } else {
+      peers_->DisableTiming();
+    }
+    return true;
+  }
   int fused_grid() const { return peers_ ? peers_->fused_grid() : 0; }
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;

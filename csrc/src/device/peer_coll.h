@@ -254,6 +254,13 @@ class PeerGroup {
   uint64_t fused_chunks() const { return fused_chunks_; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
+  /*! \brief stop timing phases (the events stay for a later EnableTiming) */
+  void DisableTiming() { timing_ = false; }
+  /*! \brief forget the phase times accumulated so far */
+  void ResetTiming() {
+    for (double &m : phase_ms_) m = 0;
+    timed_ops_ = 0;
+  }
   /*! \brief fold the last timed op into the phase totals (call after the stream drained) */
   void CollectTiming();
   static constexpr int kPhases = 5;  // stage copy, barrier, reduce, barrier, gather

@@ -420,6 +420,14 @@ def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str]
     return True
 
 
+def set_phase_timing(on: bool) -> bool:
+    """Time the phases of the direct transport's classic two-shot allreduce (stage, barrier,
+    reduce, barrier, gather) with hipEvents from now on, with fresh totals (on=True), or stop.
+    Averages per op appear in stats()["direct_phase_us"].  False without a direct transport."""
+    _check_init()
+    return _LIB.RabitDevSetPhaseTiming(1 if on else 0) == 0
+
+
 def last_error() -> str:
     if _LIB is None:
         return ""

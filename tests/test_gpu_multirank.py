@@ -147,6 +147,13 @@ def test_bench_torchrun_shared_gpu(n):
         ("direct-%s-%s" % (m, f), i) for m in ("pull", "push") for f in ("classic", "fused")
         for i in ("torch", "symmetric")}, rec["variants"]
     assert all(v["check"] and v["t_us"] > 0 for v in ran), rec["variants"]
+    # where the classic direct form's time goes, per phase, for pull and push
+    br = {b["transport"]: b for b in rec["direct_phase_breakdown"]}
+    assert set(br) == {"direct-pull-classic", "direct-push-classic"}, br
+    for b in br.values():
+        assert b["timed_ops"] == 5 and set(b["phase_us"]) == {
+            "stage", "barrier1", "reduce", "barrier2", "gather"}, b
+        assert all(t >= 0 for t in b["phase_us"].values()) and b["phase_us"]["gather"] > 0, b
 
 
 @pytest.mark.parametrize("mode", ["pull", "push"])
