@@ -128,10 +128,44 @@ def reference_measured(world, value):
     return None
 
 
+def size_sweep(rabit, torch, dev, world):
+    """N > 1: float32 sum latency from 4 KiB to 16 MiB on each transport that is up (median of
+    10, ranks in lock step, max over ranks) -- the data behind the size routing; the calibrated
+    routing is restored afterwards"""
+    st0 = rabit.stats()
+    out = {}
+    for name, which in (("rccl", rabit.TRANSPORT_RCCL), ("direct", rabit.TRANSPORT_DIRECT),
+                        ("routed", rabit.TRANSPORT_AUTO)):
+        phase("sweep %s" % name)
+        up = rabit.set_device_transport(which, None)
+        if which == rabit.TRANSPORT_DIRECT and up:
+            # the calibrated direct form
+            up = rabit.set_device_transport(which, "push" if st0.get("direct_push") else "pull",
+                                            bool(st0.get("direct_fused")))
+        up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
+        if not up:
+            continue
+        row = {}
+        for nbytes in (4 << 10, 64 << 10, 1 << 20, 16 << 20):
+            x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+            rabit.allreduce(x, rabit.SUM)
+            row[str(nbytes)] = round(_timed(rabit, torch, lambda: rabit.allreduce(x, rabit.SUM),
+                                            10) * 1e6, 1)
+        out[name + "_us"] = row
+        rabit.checkpoint(None)
+    rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
+    if st0.get("device_direct"):
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+                                   bool(st0.get("direct_fused")))
+    return out
+
+
 def run_extras(rabit, torch, dev, world):
     """BASELINE.json configs 3 and 4 plus the checkpoint cost of config 5, on this job's ranks
     (result log and checkpoint paths included, as in the headline step)."""
     out = {}
+    if world > 1:
+        out["size_sweep"] = size_sweep(rabit, torch, dev, world)
     # config 3: Broadcast of a 1 GiB blob from root 0
     nb = 1 << 30
     blob = torch.empty(nb, dtype=torch.uint8, device=dev)
