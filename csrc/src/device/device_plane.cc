@@ -414,6 +414,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_push(cfg_.direct_mode == 2);
     peers_->set_fused(cfg_.fused_mode == 1);  // auto: classic until the calibration decides
     peers_->set_fused_grid(cfg_.fused_grid);
+    peers_->set_fused_oneshot_max(cfg_.fused_oneshot_max);
     peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
   } catch (const std::exception &e) {
     peers_.reset();

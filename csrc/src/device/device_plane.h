@@ -59,6 +59,8 @@ struct DeviceConfig {
   int fused_mode{2};                   // direct two-shot chunks as one fused kernel: 0 never,
                                        // 1 always, 2 as the calibration finds faster
   int fused_grid{0};                   // workgroups of a fused launch (0: automatic)
+  size_t fused_oneshot_max{64u << 10}; // one-shot direct ops up to this size as one fused
+                                       // launch (0: never; above it the 3-launch form)
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
   size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
@@ -242,6 +244,7 @@ class DevicePlane {
   uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
   uint64_t oneshot_ops() const { return peers_ ? peers_->oneshot_ops() : 0; }
   uint64_t fused_chunks() const { return peers_ ? peers_->fused_chunks() : 0; }
+  uint64_t fused_oneshots() const { return peers_ ? peers_->fused_oneshots() : 0; }
   void SetFused(bool v) {
     if (peers_ != nullptr) peers_->set_fused(v);
   }

@@ -359,6 +359,91 @@ __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduce
   }
 }
 
+/*!
+ * \brief one-shot allreduce of a small chunk in ONE launch (instead of stage copy + barrier
+ *        kernel + reduce kernel): workgroup i stages tile i of this rank's input into its stage,
+ *        raises the tile's ready flag, waits for every rank's ready flag of that tile, then
+ *        reduces the tile from all n stages in rank order (identical bits everywhere) into out
+ *        and out2.  Stage buffers alternate by parity and a rank's next launch on the same
+ *        parity starts only after every peer raised its flags of the launch in between, which a
+ *        peer does after its reads of this one: no second hand-off is needed.  The grid is at
+ *        most a few dozen workgroups, so every one is resident.
+ */
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void FusedOneshotKernel(FusedAllreduceArgs a) {
+  __shared__ int s_bad;
+  __shared__ const char *s_in[kMaxPeers];
+  if (GroupFailed(a)) return;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  const int n = a.n, r = a.rank;
+  constexpr size_t L = 16 / sizeof(T);
+  const T alpha = static_cast<T>(a.alpha);
+  const T *src = reinterpret_cast<const T *>(a.src);
+  T *out = reinterpret_cast<T *>(a.out);
+  T *out2 = reinterpret_cast<T *>(a.out2);
+  T *mine = reinterpret_cast<T *>(a.stage[r]);
+  const bool vsrc = (reinterpret_cast<uintptr_t>(src) & 15u) == 0;
+  const bool vout = (reinterpret_cast<uintptr_t>(out) & 15u) == 0 &&
+                    (reinterpret_cast<uintptr_t>(out2) & 15u) == 0;
+  for (int i = blockIdx.x; i < a.tiles; i += gridDim.x) {
+    const size_t lo = static_cast<size_t>(i) * a.tile;
+    const size_t hi = lo + a.tile < a.count ? lo + a.tile : a.count;
+    CopyPrep<T, false>(mine + lo, src + lo, hi - lo, a.prep, alpha, vsrc);
+    Publish(a, 1, [&](int) { return ReadyFlag(a, r, i); });
+    if (!Await(a, &s_bad, n, [&](int p) { return p == r ? nullptr : ReadyFlag(a, p, i); })) {
+      return;
+    }
+    if (threadIdx.x < static_cast<unsigned>(n)) {
+      s_in[threadIdx.x] = a.stage[threadIdx.x] + lo * sizeof(T);
+    }
+    __syncthreads();
+    const size_t nvec = (hi - lo) / L;
+    for (size_t v = threadIdx.x; v < nvec; v += kBlock) {
+      uint4 x[kMaxPeers];
+#pragma unroll
+      for (int k = 0; k < kMaxPeers; ++k) {
+        if (k < n) x[k] = reinterpret_cast<const uint4 *>(s_in[k])[v];
+      }
+      const uint4 y = ReduceVecsN<T, OP, kMaxPeers>(x, n, a.post);
+      PutVec<T>(out, lo + v * L, y, vout);
+      if (out2 != nullptr) PutVec<T>(out2, lo + v * L, y, vout);
+    }
+    for (size_t e = nvec * L + threadIdx.x; e < hi - lo; e += kBlock) {
+      const T *srcs[kMaxPeers];
+      for (int k = 0; k < n; ++k) srcs[k] = reinterpret_cast<const T *>(s_in[k]);
+      const T y = ReduceScalarN<T, OP>(srcs, n, e, a.post);
+      out[lo + e] = y;
+      if (out2 != nullptr) out2[lo + e] = y;
+    }
+    __syncthreads();  // s_in is rewritten by the next tile
+  }
+}
+
+template <typename T>
+hipError_t LaunchOneshotT(const FusedAllreduceArgs &args, int grid, hipStream_t st) {
+  switch (args.op) {
+    case kOpMax:
+      hipLaunchKernelGGL((FusedOneshotKernel<T, kOpMax>), dim3(grid), dim3(kBlock), 0, st, args);
+      break;
+    case kOpMin:
+      hipLaunchKernelGGL((FusedOneshotKernel<T, kOpMin>), dim3(grid), dim3(kBlock), 0, st, args);
+      break;
+    case kOpSum:
+      hipLaunchKernelGGL((FusedOneshotKernel<T, kOpSum>), dim3(grid), dim3(kBlock), 0, st, args);
+      break;
+    case kOpOr:
+      if constexpr (std::is_integral<T>::value) {
+        hipLaunchKernelGGL((FusedOneshotKernel<T, kOpOr>), dim3(grid), dim3(kBlock), 0, st,
+                           args);
+        break;
+      }
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t LaunchT(const FusedAllreduceArgs &args, int grid, hipStream_t st) {
   switch (args.op) {
@@ -405,6 +490,33 @@ int FusedResidentBlocks(int device) {
   take(reinterpret_cast<const void *>(&FusedAllreduceKernel<bf16_t, kOpSum>));
   take(reinterpret_cast<const void *>(&FusedAllreduceKernel<int8_t, kOpOr>));
   return cus * per_cu;
+}
+
+hipError_t LaunchFusedOneshot(const FusedAllreduceArgs &args, int grid, hipStream_t stream) {
+  if (args.n < 1 || args.n > kMaxPeers || args.rank < 0 || args.rank >= args.n || grid < 1 ||
+      args.tiles < 1 || args.tiles > args.tiles_cap || args.tile % 256 != 0 ||
+      args.count > args.tile * static_cast<size_t>(args.tiles) || args.push || args.zero_copy) {
+    return hipErrorInvalidValue;
+  }
+  if (args.post != 0.0 && args.dtype != 6 && args.dtype != 7 && args.dtype != 10 &&
+      args.dtype != 11) {
+    return hipErrorInvalidValue;
+  }
+  switch (args.dtype) {
+    case 0: return LaunchOneshotT<int8_t>(args, grid, stream);
+    case 1: return LaunchOneshotT<uint8_t>(args, grid, stream);
+    case 2: return LaunchOneshotT<int32_t>(args, grid, stream);
+    case 3: return LaunchOneshotT<uint32_t>(args, grid, stream);
+    case 4:
+    case 8: return LaunchOneshotT<int64_t>(args, grid, stream);
+    case 5:
+    case 9: return LaunchOneshotT<uint64_t>(args, grid, stream);
+    case 6: return LaunchOneshotT<float>(args, grid, stream);
+    case 7: return LaunchOneshotT<double>(args, grid, stream);
+    case 10: return LaunchOneshotT<half_t>(args, grid, stream);
+    case 11: return LaunchOneshotT<bf16_t>(args, grid, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t LaunchFusedAllreduce(const FusedAllreduceArgs &args, int grid, hipStream_t stream) {

@@ -136,6 +136,9 @@ inline size_t FusedFlagWords(int tiles_cap) {
 int FusedResidentBlocks(int device);
 /*! \brief enqueue the fused allreduce of one chunk on `grid` workgroups */
 hipError_t LaunchFusedAllreduce(const FusedAllreduceArgs &args, int grid, hipStream_t stream);
+/*! \brief enqueue a small chunk's one-shot allreduce as one launch (tiles of args.tile elements
+ *  over args.count; stage copy, per-tile ready flags, reduce of all n stages into out / out2) */
+hipError_t LaunchFusedOneshot(const FusedAllreduceArgs &args, int grid, hipStream_t stream);
 
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
                              const volatile int *abort_word, int *dev_status, int *host_status,
@@ -245,6 +248,10 @@ class PeerGroup {
    *        FusedAllreduceArgs) instead of stage + barrier + reduce + barrier + gather launches
    */
   void set_fused(bool v) { fused_ = v; }
+  /*! \brief one-shot ops of at most this many bytes as one fused launch, larger ones (and all
+   *  with 0) as stage copy + barrier + reduce */
+  void set_fused_oneshot_max(size_t b) { fused_oneshot_max_ = b; }
+  uint64_t fused_oneshots() const { return fused_oneshots_; }
   bool fused() const { return fused_; }
   /*! \brief workgroups of a fused launch (0: automatic, from the ranks sharing a GPU) */
   void set_fused_grid(int g) { fused_grid_req_ = g; }
@@ -319,6 +326,8 @@ class PeerGroup {
   bool push_{false};
   uint64_t push_chunks_{0};
   bool fused_{true};
+  size_t fused_oneshot_max_{64u << 10};
+  uint64_t fused_oneshots_{0};
   int fused_grid_req_{0}, fused_grid_{256};
   size_t fused_min_bytes_{0};
   int tiles_cap_{0};                // flag slots per array of a fused flag block

@@ -103,6 +103,11 @@ void EngineBase::SetParam(const char *name, const char *val) {
     dcfg_.fused_mode = !strcmp(val, "auto") ? 2 : (utils::StringToBool(val) ? 1 : 0);
   }
   if (is("rabit_device_fused_grid")) dcfg_.fused_grid = atoi(val);
+  if (is("rabit_device_fused_oneshot")) {
+    // a size (one-shot ops up to it in one launch), or a boolean (0: never, 1: the default 64K)
+    const size_t v = core::ParseUnit(name, val);
+    dcfg_.fused_oneshot_max = v == 1 ? (64u << 10) : v;
+  }
   if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
   if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
@@ -692,6 +697,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
      << ",\"oneshot_ops\":" << (dev_ ? dev_->oneshot_ops() : 0)
      << ",\"fused_chunks\":" << (dev_ ? dev_->fused_chunks() : 0)
+     << ",\"fused_oneshots\":" << (dev_ ? dev_->fused_oneshots() : 0)
      << ",\"fused_grid\":" << (dev_ ? dev_->fused_grid() : 0)
      << ",\"symmetric_heap_used\":" << (dev_ ? dev_->sym_heap_used() : 0)
      << ",\"device_direct_min\":"

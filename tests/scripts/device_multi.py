@@ -117,6 +117,8 @@ assert torch.equal(buf.cpu(), exp), "allgatherv"
 stats = rabit.stats()
 assert stats["device_direct"] == 1 and stats["device_rccl"] == 0, stats
 assert stats["oneshot_ops"] > 0, stats  # the small cases took the one-shot path
+fused_oneshot = not any(a == "rabit_device_fused_oneshot=0" for a in sys.argv[1:])
+assert (stats["fused_oneshots"] > 0) == fused_oneshot, stats  # ...in the form asked for
 if "rabit_device_direct_mode=push" in sys.argv:
     assert stats["direct_push"] == 1 and stats["push_chunks"] > 0, stats
 

@@ -24,10 +24,12 @@ def _run(script, nworker, args=(), attempts=1, timeout=300, env=None):
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_direct_collectives(world, fused):
-    """fused=1: two-shot chunks as one kernel with per-tile hand-offs; 0: the 5-launch form"""
+    """fused=1: two-shot chunks as one kernel with per-tile hand-offs and small ops as one
+    one-shot kernel; 0: the 5-launch two-shot form and the 3-launch one-shot form"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("device_multi.py", world, ["rabit_device_fused=" + fused])
+    rc, out = _run("device_multi.py", world, ["rabit_device_fused=" + fused,
+                                              "rabit_device_fused_oneshot=" + fused])
     assert rc == 0, out[-5000:]
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
@@ -51,7 +53,8 @@ def test_direct_recovery(mock, mode, fused):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     rc, out = _run("device_ft.py", 3, mock + ["rabit_device_direct_mode=" + mode,
-                                              "rabit_device_fused=" + fused], attempts=4)
+                                              "rabit_device_fused=" + fused,
+                                              "rabit_device_fused_oneshot=" + fused], attempts=4)
     assert rc == 0, out[-5000:]
     assert out.count("DEVFT OK") == 3, out[-3000:]
     if mock:

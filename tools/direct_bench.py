@@ -32,6 +32,9 @@ def main():
     sizes = (256 << 10, 1 << 20, 4 << 20, 16 << 20, 32 << 20, 128 << 20)
     if sym:
         sizes = (1 << 20, 8 << 20, 128 << 20)  # bump-allocated heap: keep the total small
+    if os.environ.get("XR_SIZES"):
+        sizes = tuple(int(v) for v in os.environ["XR_SIZES"].split(","))
+    reps = int(os.environ.get("XR_REPS", "10"))
     for nbytes in sizes:
         if sym:
             x = rabit.symmetric_empty(nbytes // 4)
@@ -42,7 +45,7 @@ def main():
             rabit.allreduce(x, rabit.SUM)
         times = []
         before = rabit.stats()
-        for _ in range(10):
+        for _ in range(reps):
             torch.cuda.synchronize()
             rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)  # host barrier
             t0 = time.perf_counter()
@@ -62,6 +65,7 @@ def main():
             print(json.dumps({
                 "world_on_one_gpu": world, "bytes": nbytes, "symmetric": sym, "t_us": round(med * 1e6, 1),
                 "fused": fused == "1", "fused_chunks": st.get("fused_chunks", 0),
+                "fused_oneshots": st.get("fused_oneshots", 0),
                 "direct_push": st.get("direct_push", 0),
                 "phase_us": phase, "timed_ops": n1 - n0,
             }), flush=True)
