@@ -12,6 +12,7 @@ in place over RCCL/xGMI and the CDNA4 kernels, ordered on torch's current stream
 from __future__ import annotations
 
 import ctypes
+import threading
 import json
 import pickle
 import sys
@@ -93,6 +94,7 @@ def init(args: Optional[Sequence] = None, lib: str = "standard", lib_dll=None, *
     args = [a if isinstance(a, bytes) else str(a).encode() for a in args]
     args += [("%s=%s" % (k, v)).encode() for k, v in params.items()]
     _loadlib(lib, lib_dll)
+    _GENERATION[0] += 1
     arr = (ctypes.c_char_p * len(args))(*args)
     if not _LIB.RabitInit(len(args), arr):
         raise RuntimeError("rabit init failed: %s" % last_error())
@@ -103,6 +105,7 @@ def finalize():
     if _LIB is None:
         return
     _LIB.RabitFinalize()
+    _GENERATION[0] += 1
     _unloadlib()
 
 
@@ -170,12 +173,31 @@ def _is_torch(x) -> bool:
         isinstance(x, sys.modules["torch"].Tensor)
 
 
-def _sync_stream_for(t):
-    """Order device collectives after torch's current stream on t's device."""
+# the stream last passed to the engine, per thread (an engine belongs to one thread) and per
+# init generation (a new engine starts on the default stream)
+_STREAM_CACHE = threading.local()
+_GENERATION = [0]
+
+
+def _current_raw_stream(device):
+    """torch's current HIP stream on `device` as an integer handle (the raw accessor costs
+    ~0.2 us against ~2 us for torch.cuda.current_stream(...).cuda_stream)"""
     import torch
 
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return raw(device.index if device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _sync_stream_for(t):
+    """Order device collectives after torch's current stream on t's device (the engine is told
+    only when the stream changed since the last call)."""
     if t.is_cuda:
-        _LIB.RabitSetStream(ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream))
+        s = (_GENERATION[0], _current_raw_stream(t.device))
+        if getattr(_STREAM_CACHE, "last", None) != s:
+            _LIB.RabitSetStream(ctypes.c_void_p(s[1]))
+            _STREAM_CACHE.last = s
 
 
 def allreduce(data, op: int, prepare_fun: Optional[Callable] = None):
@@ -210,9 +232,15 @@ def allreduce(data, op: int, prepare_fun: Optional[Callable] = None):
     return buf
 
 
+_NO_PREPARE = {}
+
+
 def _make_prepare(prepare_fun, data):
     if prepare_fun is None:
-        return _LIB.PREPARE_FN()
+        cb = _NO_PREPARE.get(id(_LIB))
+        if cb is None:
+            cb = _NO_PREPARE[id(_LIB)] = _LIB.PREPARE_FN()
+        return cb
 
     def pfunc(_arg):
         prepare_fun(data)
