@@ -350,8 +350,12 @@ def main():
     # N > 1: RCCL's channel (CTA) count is timed at start-up against fixed counts and the
     # fastest communicator is kept (transport.rccl_tuning)
     tune = {"rabit_rccl_tune": "1"} if world > 1 and args.rccl_tune else {}
+    # the robust engine logs every result until the next checkpoint: reserve the HBM log for
+    # the check, warmup and timed steps up front (one allocation), as a job would size it for
+    # the results of one iteration, so the timed loop never waits on hipMalloc
+    log = {"rabit_device_log_reserve": str((args.warmup + args.steps + 3) * n * 4)}
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
-                        rabit_world1_fastpath=0, rabit_device=gpu, **heap, **tune)
+                        rabit_world1_fastpath=0, rabit_device=gpu, **heap, **tune, **log)
     dev = torch.device("cuda", gpu)
 
     phase("reference")

@@ -99,17 +99,32 @@ void *DeviceArena::Alloc(size_t bytes) {
     if (cur_ + 1 == chunks_.size()) break;
     ++cur_;
   }
-  if (reserved() + std::max(need, chunk_) > cap_) return nullptr;
+  const size_t have = reserved();
+  const size_t least = std::max(need, chunk_);
+  if (have + least > cap_) return nullptr;
+  size_t want = least;
+  if (chunks_.empty()) {
+    want = std::max(want, reserve_);
+  } else if (!pinned_) {
+    want = std::max(want, std::min(have, kMaxStep));  // geometric growth of the HBM log
+  }
+  want = std::min(want, cap_ - have);
   Chunk c;
-  c.size = std::max(need, chunk_);
   c.used = need;
   void *base = nullptr;
-  const hipError_t e =
-      pinned_ ? hipHostMalloc(&base, c.size, hipHostMallocDefault) : hipMalloc(&base, c.size);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
+  auto try_alloc = [&](size_t size) {
+    const hipError_t e =
+        pinned_ ? hipHostMalloc(&base, size, hipHostMallocDefault) : hipMalloc(&base, size);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      base = nullptr;
+      return false;
+    }
+    c.size = size;
+    return true;
+  };
+  // the larger step first; when memory is short, the smallest chunk that fits this slot
+  if (!try_alloc(want) && (want == least || !try_alloc(least))) return nullptr;
   c.base = static_cast<char *>(base);
   chunks_.push_back(c);
   cur_ = chunks_.size() - 1;
@@ -171,7 +186,7 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   stream_ = cfg_.ops_on_user_stream ? user_stream_ : own_stream_;
   CheckHip(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
   CheckHip(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
-  arena_.Configure(cfg.arena_chunk, cfg.arena_cap);
+  arena_.Configure(cfg.arena_chunk, cfg.arena_cap, false, cfg.arena_reserve);
   spill_.Configure(std::min<size_t>(cfg.arena_chunk, 64u << 20), cfg.spill_cap, true);
   if (cfg.sym_heap > 0) {
     // symmetric heap: uncached like the stage buffers (peers read it over xGMI in place)

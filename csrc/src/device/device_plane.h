@@ -42,6 +42,7 @@ struct DeviceConfig {
   double op_timeout_sec{-1};           // deadline of a device op: < 0 auto (size-scaled), 0 none
   double drain_timeout_sec{30};        // after an abort, the stream must drain within this
   size_t arena_chunk{256u << 20};      // result-log arena growth step
+  size_t arena_reserve{0};             // first result-log chunk (0: arena_chunk)
   size_t arena_cap{size_t(64) << 30};  // HBM result-log cap; beyond it (or when hipMalloc fails)
                                        // results spill to pinned host memory
   size_t spill_cap{size_t(1) << 40};   // pinned host bytes the result log may spill (0: no spill,
@@ -79,11 +80,17 @@ inline double AutoOpDeadline(size_t bytes) { return 60.0 + static_cast<double>(b
 class DeviceArena {
  public:
   ~DeviceArena();
-  void Configure(size_t chunk, size_t cap, bool pinned = false) {
+  /*! \brief chunk: smallest growth step; reserve: size of the first chunk (one allocation up
+   *  front instead of many during the first iterations); HBM arenas then grow geometrically
+   *  (each new chunk as large as everything reserved so far, at most kMaxStep), so a long
+   *  stretch between checkpoints costs O(log) hipMallocs, not one per chunk */
+  void Configure(size_t chunk, size_t cap, bool pinned = false, size_t reserve = 0) {
     chunk_ = chunk;
     cap_ = cap;
     pinned_ = pinned;
+    reserve_ = reserve;
   }
+  static constexpr size_t kMaxStep = size_t(8) << 30;
   bool pinned() const { return pinned_; }
   /*! \brief 256-byte aligned slot, nullptr when over the cap or out of memory */
   void *Alloc(size_t bytes);
@@ -100,7 +107,7 @@ class DeviceArena {
   };
   std::vector<Chunk> chunks_;
   size_t cur_{0};
-  size_t chunk_{256u << 20}, cap_{size_t(64) << 30};
+  size_t chunk_{256u << 20}, cap_{size_t(64) << 30}, reserve_{0};
   bool pinned_{false};
 };
 

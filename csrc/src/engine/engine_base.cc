@@ -74,6 +74,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_log_cap")) dcfg_.arena_cap = core::ParseUnit(name, val);
   if (is("rabit_device_spill_cap")) dcfg_.spill_cap = core::ParseUnit(name, val);
   if (is("rabit_device_log_chunk")) dcfg_.arena_chunk = core::ParseUnit(name, val);
+  if (is("rabit_device_log_reserve")) dcfg_.arena_reserve = core::ParseUnit(name, val);
   if (is("rabit_device_algo")) {
     const std::string v(val);
     if (v == "auto") {
