@@ -234,3 +234,15 @@ def test_rccl_init_failure_falls_back_to_direct():
     assert rc == 0, out[-5000:]
     assert out.count("DEVMULTI OK") == 2, out[-3000:]
     assert "running on the direct transport alone" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_small_op_stress(world):
+    """thousands of back-to-back small allreduces (fused one-shot, classic one-shot, two-shot),
+    values changing every op, results checked: a rank overwriting a stage buffer a slower peer
+    still reads would show up as a wrong sum"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("oneshot_stress.py", world, ["1500", "rabit_device_fused=1"], timeout=240)
+    assert rc == 0, out[-5000:]
+    assert out.count("STRESS OK") == world, out[-3000:]
