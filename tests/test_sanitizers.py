@@ -2,6 +2,7 @@
 UBSan and with ThreadSanitizer (`make asan`, `make tsan`; device code is not instrumented),
 running the C++ unit tests (watchdog thread included) and a multi-process recovery scenario
 with worker deaths.  Any sanitizer report fails the test."""
+import fcntl
 import os
 import subprocess
 import sys
@@ -15,8 +16,13 @@ REPORTS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitize
 
 
 def _build(kind):
-    subprocess.check_call(["make", "-j8", kind], cwd=ROOT, stdout=subprocess.DEVNULL,
-                          stderr=subprocess.DEVNULL)
+    # two test processes (pytest -n) building the same flavour would race on its object
+    # directory: one make per flavour at a time
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".%s.lock" % kind), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-j8", kind], cwd=ROOT, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.DEVNULL)
     return os.path.join(ROOT, "build", kind, "bin")
 
 
