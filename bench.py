@@ -21,7 +21,10 @@ engine's bookkeeping plus its HBM result-log copy (rabit_world1_fastpath=0), rep
 Rank 0 prints one JSON line.  `value` is the whole-job aggregate throughput N * S / t
 (GB/s, S = 128 MiB per rank, weak scaling); nccl-tests style `busbw_GBps` / `algbw_GBps` and
 the per-step wall clock are reported alongside.  The whole run is under a wall-clock deadline
-(--deadline): a rank that exceeds it names the phase it was in and exits non-zero.
+(--deadline): a rank that exceeds it names the phase it was in and exits non-zero.  The side
+measurements after the headline (variants, extras) have a budget of their own (--post-deadline)
+and cannot take the measured headline with them: an exception in one is recorded in
+`post_headline_failure`, and a rank stuck in one ends the run with the headline printed.
 """
 import argparse
 import json
@@ -42,18 +45,49 @@ def phase(name):
     PHASE["name"] = name
 
 
-def start_deadline(seconds, rank):
-    """exit non-zero, naming the phase, if the run is not done within `seconds`"""
-    def expire():
-        sys.stderr.write("bench.py: rank %d exceeded its %d s deadline in phase '%s' "
-                         "(%.0f s into the run)\n" % (rank, seconds, PHASE["name"],
-                                                       time.time() - PHASE["t0"]))
+def start_deadline(seconds, rank, post_seconds):
+    """exit non-zero, naming the phase, if the run is not done within `seconds`.  Once the
+    headline is measured (HEADLINE["rec"] set), the phases after it (variants, extras) get
+    `post_seconds` more at most; if they overrun, or a rank hangs in them, rank 0 still prints
+    the measured headline once (flagged with the phase that did not finish) and the run exits 0:
+    a broken side measurement must not take the headline with it."""
+    def watch():
+        while True:
+            now = time.time()
+            rec = HEADLINE["rec"]
+            limit = PHASE["t0"] + seconds
+            if rec is not None:
+                limit = min(limit, HEADLINE["t"] + post_seconds)
+            if now >= limit:
+                break
+            time.sleep(min(1.0, limit - now))
+        sys.stderr.write("bench.py: rank %d exceeded its deadline in phase '%s' "
+                         "(%.0f s into the run)\n" % (rank, PHASE["name"], time.time() - PHASE["t0"]))
         sys.stderr.flush()
+        if HEADLINE["rec"] is not None:
+            emit_headline("deadline in phase '%s'" % PHASE["name"])
+            os._exit(0)
         os._exit(3)
-    t = threading.Timer(seconds, expire)
-    t.daemon = True
+    t = threading.Thread(target=watch, daemon=True)
     t.start()
     return t
+
+
+HEADLINE = {"rec": None, "t": 0.0, "printed": False, "rank": 0}
+PRINT_LOCK = threading.Lock()
+
+
+def emit_headline(failure=None):
+    """rank 0 prints the one JSON line, exactly once (main thread or deadline watcher)"""
+    with PRINT_LOCK:
+        if HEADLINE["printed"] or HEADLINE["rec"] is None:
+            return
+        HEADLINE["printed"] = True
+        rec = HEADLINE["rec"]
+        if failure is not None:
+            rec["post_headline_failure"] = failure
+        if HEADLINE["rank"] == 0:
+            print(json.dumps(rec), flush=True)
 
 
 def pattern_fill(x, rank):
@@ -320,6 +354,9 @@ def main():
                          "start-up and keep the fastest")
     ap.add_argument("--deadline", type=int, default=600,
                     help="wall-clock limit of the whole run in seconds")
+    ap.add_argument("--post-deadline", type=int, default=240,
+                    help="seconds the phases after the headline (variants, extras) may take "
+                         "before rank 0 prints the headline alone and the run ends")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -328,7 +365,7 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: launch N>1 with "
                          "torch.distributed.run" % (args.gpus, world))
-    timer = start_deadline(args.deadline, rank)
+    start_deadline(args.deadline, rank, args.post_deadline)
     phase("import")
     import torch
     import rabit_amd as rabit
@@ -395,16 +432,6 @@ def main():
     elapsed = time_steps(rabit, torch, x, args.steps)
     st_head = rabit.stats()
 
-    variants = phases = None
-    if world > 1 and args.variants:
-        phase("variants")
-        rabit.checkpoint(None)
-        variants, phases = run_variants(rabit, torch, dev, n, world, rank, ref,
-                                        max(5, args.steps // 2),
-                                        forced_rccl=check_fallback is not None)
-    phase("extras")
-    extras = run_extras(rabit, torch, dev, world) if args.extras else {}
-
     t_step = elapsed / args.steps
     size_bytes = n * 4
     algbw = size_bytes / t_step / 1e9
@@ -454,9 +481,9 @@ def main():
                       "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),
                       "peer_links": st.get("peer_links"),
                       "rccl_tuning": st.get("rccl_tuning")},
-        "variants": variants,
-        "direct_phase_breakdown": phases,
-        "extras": extras,
+        "variants": None,
+        "direct_phase_breakdown": None,
+        "extras": None,
         "reference_measured": reference_measured(world, aggregate),
     }
     if world == 1:
@@ -465,12 +492,32 @@ def main():
                           "not a collective)")
     if shared_gpu:
         rec["shared_gpu_rehearsal"] = "%d ranks on %d GPU(s): not an xGMI measurement" % (world, ngpu)
-    if rank == 0:
-        print(json.dumps(rec), flush=True)
+    HEADLINE["rank"] = rank
+    HEADLINE["t"] = time.time()
+    HEADLINE["rec"] = rec
+
+    # side measurements after the headline: an exception is recorded, not fatal (a rank stuck
+    # in one is cut off by the post-headline deadline, which still prints the headline)
+    failures = []
+    if world > 1 and args.variants:
+        phase("variants")
+        try:
+            rabit.checkpoint(None)
+            rec["variants"], rec["direct_phase_breakdown"] = run_variants(
+                rabit, torch, dev, n, world, rank, ref, max(5, args.steps // 2),
+                forced_rccl=check_fallback is not None)
+        except Exception as e:  # noqa: BLE001 - reported in the record
+            failures.append("variants: %s: %s" % (type(e).__name__, e))
+    if args.extras:
+        phase("extras")
+        try:
+            rec["extras"] = run_extras(rabit, torch, dev, world)
+        except Exception as e:  # noqa: BLE001
+            failures.append("extras: %s: %s" % (type(e).__name__, e))
+    emit_headline("; ".join(failures) if failures else None)
     phase("finalize")
     del x
     ctx.finalize()
-    timer.cancel()
 
 
 if __name__ == "__main__":
