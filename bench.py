@@ -498,7 +498,9 @@ def main():
 
     # side measurements after the headline: an exception is recorded, not fatal (a rank stuck
     # in one is cut off by the post-headline deadline, which still prints the headline)
+    # native errors raise from here on instead of exiting the process (set_error_mode)
     failures = []
+    rabit.set_error_mode(True)
     if world > 1 and args.variants:
         phase("variants")
         try:
@@ -508,7 +510,9 @@ def main():
                 forced_rccl=check_fallback is not None)
         except Exception as e:  # noqa: BLE001 - reported in the record
             failures.append("variants: %s: %s" % (type(e).__name__, e))
-    if args.extras:
+    if args.extras and failures:
+        failures.append("extras: skipped after the variants failed")
+    elif args.extras:
         phase("extras")
         try:
             rec["extras"] = run_extras(rabit, torch, dev, world)
