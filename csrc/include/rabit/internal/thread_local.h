@@ -1,19 +1,23 @@
 /*!
  * \file thread_local.h
- * \brief Per-thread singleton holder (parity: reference `include/rabit/internal/thread_local.h:38-85`).
- *        C++11 `thread_local` gives destruction at thread exit, so no registry is needed.
+ * \brief ThreadLocalStore<T>::Get(): one lazily built T per calling thread, destroyed when the
+ *        thread exits (API of the reference's include/rabit/internal/thread_local.h:38-85).
+ *        The reference keeps a registry of heap objects for pre-C++11 compilers; here the
+ *        object is a function-local `thread_local`, so there is nothing to register or free.
  */
 #ifndef RABIT_INTERNAL_THREAD_LOCAL_H_
 #define RABIT_INTERNAL_THREAD_LOCAL_H_
 
 namespace rabit {
-/*! \brief one lazily constructed T per thread */
 template <typename T>
-class ThreadLocalStore {
- public:
-  static T *Get() {
-    static thread_local T inst;
-    return &inst;
+struct ThreadLocalStore {
+  /*! \brief this thread's instance (constructed on first use) */
+  static T *Get() { return &Slot(); }
+
+ private:
+  static T &Slot() {
+    thread_local T value{};
+    return value;
   }
 };
 }  // namespace rabit
