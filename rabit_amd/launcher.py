@@ -1,4 +1,5 @@
-"""Local job launcher with restart-on-failure (the role of `dmlc-submit --cluster local`).
+"""Job launcher with restart-on-failure (the role of `dmlc-submit --cluster local|ssh`, which
+the reference's test/test.mk and guide use).
 
 Starts a tracker, spawns `num_workers` copies of a command with the DMLC_* environment and
 restarts any worker that exits with a non-zero status, up to `num_attempt` times, passing the
@@ -6,16 +7,27 @@ attempt number in DMLC_NUM_ATTEMPT (the mock engine keys its kill points on it).
 the fault-tolerance scenarios of the reference's test/test.mk run on one machine.
 
     python -m rabit_amd.launcher -n 10 --num-attempt 20 -- ./model_recover 10000 mock=0,0,1,0
+
+Multi-node jobs (`--cluster ssh --host-file hosts`): workers are started over ssh on the hosts
+of the file, `host[:slots]` or `host slots=N` per line.  Ranks fill each host's slots before the
+next host, so ranks that share a node are consecutive (their ring links and the direct device
+transport stay on xGMI); every worker gets LOCAL_RANK / LOCAL_WORLD_SIZE for its node, from
+which the device plane picks its GPU (one process per GPU).  The tracker listens on --host-ip,
+by default this host's address.
+
+    python -m rabit_amd.launcher --cluster ssh --host-file hosts -n 16 -- python train.py
 """
 from __future__ import annotations
 
 import argparse
 import os
+import shlex
+import socket
 import subprocess
 import sys
 import threading
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from .tracker import RabitTracker
 
@@ -57,17 +69,20 @@ class LocalJob:
         })
         return e
 
+    def _spawn(self, task: int, attempt: int) -> subprocess.Popen:
+        return subprocess.Popen(
+            self.cmd, env=self._worker_env(task, attempt),
+            stdout=subprocess.PIPE if self.capture else None,
+            stderr=subprocess.STDOUT if self.capture else None,
+            text=self.capture)
+
     def _run_worker(self, task: int):
         attempt = 0
         while True:
             with self._lock:
                 if self._stop:
                     return
-                p = subprocess.Popen(
-                    self.cmd, env=self._worker_env(task, attempt),
-                    stdout=subprocess.PIPE if self.capture else None,
-                    stderr=subprocess.STDOUT if self.capture else None,
-                    text=self.capture)
+                p = self._spawn(task, attempt)
                 self._procs[task] = p
             if self.capture:
                 for line in p.stdout:
@@ -114,12 +129,114 @@ class LocalJob:
                     p.kill()
 
 
+def parse_host_file(path: str) -> List[Tuple[str, int]]:
+    """`host`, `host:slots` or `host slots=N` per line ('#' starts a comment)"""
+    hosts = []
+    with open(path) as f:
+        for line in f:
+            line = line.split("#", 1)[0].strip()
+            if not line:
+                continue
+            slots = 1
+            parts = line.split()
+            host = parts[0]
+            for opt in parts[1:]:
+                if opt.startswith("slots="):
+                    slots = int(opt[len("slots="):])
+            if ":" in host:
+                host, n = host.rsplit(":", 1)
+                slots = int(n)
+            if slots < 1:
+                raise ValueError("%s: host %s has no slots" % (path, host))
+            hosts.append((host, slots))
+    if not hosts:
+        raise ValueError("%s lists no hosts" % path)
+    return hosts
+
+
+def place_workers(hosts: Sequence[Tuple[str, int]], n: int) -> List[Tuple[str, int, int]]:
+    """(host, local_rank, local_world) of each task: every host's slots are filled before the
+    next host's, so the ranks of one node are consecutive"""
+    total = sum(s for _, s in hosts)
+    if n > total:
+        raise ValueError("%d workers but the host file has %d slots" % (n, total))
+    out: List[Tuple[str, int, int]] = []
+    for host, slots in hosts:
+        k = min(slots, n - len(out))
+        out.extend((host, i, k) for i in range(k))
+        if len(out) == n:
+            break
+    return out
+
+
+class SSHJob(LocalJob):
+    """A rabit job whose workers run on remote hosts over ssh (dmlc-submit --cluster ssh).
+
+    The worker's environment is not inherited across ssh: the DMLC_* / rabit_* variables, the
+    tracker address, LOCAL_RANK / LOCAL_WORLD_SIZE and the --env pairs are exported explicitly
+    in the remote shell, which changes to `workdir` (the launch directory by default, assumed
+    to be shared or replicated) before running the command.  A worker whose ssh session ends
+    with a non-zero status is restarted on the same host, like a local one."""
+
+    def __init__(self, cmd: Sequence[str], hosts: Sequence[Tuple[str, int]], num_workers: int,
+                 num_attempt: int = 1, env: Optional[Dict[str, str]] = None,
+                 host_ip: Optional[str] = None, tracker_port: int = 9091,
+                 timeout: Optional[float] = None, capture: bool = False, print_fn=None,
+                 ssh: Sequence[str] = ("ssh", "-o", "StrictHostKeyChecking=no",
+                                       "-o", "BatchMode=yes"),
+                 workdir: Optional[str] = None):
+        super().__init__(cmd, num_workers, num_attempt, env, host_ip or default_host_ip(),
+                         tracker_port, timeout, capture, print_fn)
+        self.placement = place_workers(hosts, num_workers)
+        self.ssh = list(ssh)
+        self.workdir = workdir or os.getcwd()
+
+    def _remote_env(self, task: int, attempt: int) -> Dict[str, str]:
+        host, local_rank, local_world = self.placement[task]
+        e = {k: v for k, v in self._worker_env(task, attempt).items()
+             if k.startswith(("DMLC_", "rabit_", "XRABIT_")) or k == "PYTHONPATH"}
+        e.update(self.env)
+        e.update({"LOCAL_RANK": str(local_rank), "LOCAL_WORLD_SIZE": str(local_world)})
+        return e
+
+    def remote_command(self, task: int, attempt: int) -> str:
+        exports = " ".join("%s=%s" % (k, shlex.quote(v))
+                           for k, v in sorted(self._remote_env(task, attempt).items()))
+        return "cd %s && env %s %s" % (shlex.quote(self.workdir), exports,
+                                       " ".join(shlex.quote(c) for c in self.cmd))
+
+    def _spawn(self, task: int, attempt: int) -> subprocess.Popen:
+        host = self.placement[task][0]
+        return subprocess.Popen(
+            self.ssh + [host, self.remote_command(task, attempt)],
+            stdout=subprocess.PIPE if self.capture else None,
+            stderr=subprocess.STDOUT if self.capture else None,
+            text=self.capture)
+
+
+def default_host_ip() -> str:
+    """an address of this host other peers can reach (the tracker binds and advertises it)"""
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.connect(("10.255.255.255", 1))  # no packet is sent: picks the outgoing interface
+            return s.getsockname()[0]
+    except OSError:
+        return socket.gethostbyname(socket.gethostname())
+
+
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="launch a local xrabit job")
+    ap = argparse.ArgumentParser(description="launch an xrabit job (local or over ssh)")
     ap.add_argument("-n", "--num-workers", type=int, required=True)
     ap.add_argument("--num-attempt", "--local-num-attempt", type=int, default=1,
                     help="restarts allowed per worker (fault-tolerance tests)")
-    ap.add_argument("--host-ip", default="127.0.0.1")
+    ap.add_argument("--cluster", choices=["local", "ssh"], default="local")
+    ap.add_argument("--host-file", help="--cluster ssh: host[:slots] per line")
+    ap.add_argument("--ssh", default="ssh -o StrictHostKeyChecking=no -o BatchMode=yes",
+                    help="--cluster ssh: the ssh command (host and remote command appended)")
+    ap.add_argument("--workdir", default=None,
+                    help="--cluster ssh: directory the remote workers start in (default: cwd)")
+    ap.add_argument("--host-ip", default=None,
+                    help="tracker address (default 127.0.0.1 local, this host's address ssh)")
     ap.add_argument("--port", type=int, default=9091)
     ap.add_argument("--timeout", type=float, default=None)
     ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for every worker")
@@ -129,8 +246,15 @@ def main(argv=None):
     if not cmd:
         ap.error("missing worker command")
     env = dict(kv.split("=", 1) for kv in args.env)
-    job = LocalJob(cmd, args.num_workers, args.num_attempt, env, args.host_ip, args.port,
-                   args.timeout)
+    if args.cluster == "ssh":
+        if not args.host_file:
+            ap.error("--cluster ssh needs --host-file")
+        job = SSHJob(cmd, parse_host_file(args.host_file), args.num_workers, args.num_attempt,
+                     env, args.host_ip, args.port, args.timeout, ssh=shlex.split(args.ssh),
+                     workdir=args.workdir)
+    else:
+        job = LocalJob(cmd, args.num_workers, args.num_attempt, env,
+                       args.host_ip or "127.0.0.1", args.port, args.timeout)
     rc = job.run()
     sys.exit(rc)
 

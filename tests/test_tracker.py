@@ -1,5 +1,6 @@
 """Tracker topology and launcher behaviour."""
 import os
+import re
 import subprocess
 import sys
 
@@ -102,3 +103,38 @@ def test_speed_test_cpu(native_build):
                          capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert out.returncode == 0, out.stderr
     assert "sum_tdiff-speed" in out.stdout and "bcast_tdiff-speed" in out.stdout
+
+
+def test_launcher_ssh_cluster(tmp_path):
+    """--cluster ssh: workers placed host by host (consecutive ranks share a node), started
+    through the ssh command with an explicit environment (the stand-in gives them a clean one),
+    LOCAL_RANK / LOCAL_WORLD_SIZE per node, and a killed worker restarted on its host."""
+    from rabit_amd.launcher import SSHJob, parse_host_file, place_workers
+
+    hf = tmp_path / "hosts"
+    hf.write_text("# test cluster\nnodeA:2\nnodeB slots=3\n")
+    hosts = parse_host_file(str(hf))
+    assert hosts == [("nodeA", 2), ("nodeB", 3)]
+    assert place_workers(hosts, 4) == [("nodeA", 0, 2), ("nodeA", 1, 2), ("nodeB", 0, 2),
+                                       ("nodeB", 1, 2)]
+    with pytest.raises(ValueError):
+        place_workers(hosts, 6)
+    fake = os.path.join(ROOT, "tests", "scripts", "fake_ssh.sh")
+    worker = os.path.join(ROOT, "tests", "scripts", "ssh_worker.py")
+    flag = tmp_path / "killed"
+    # task 3 dies once before rabit.init (a lost node process); the launcher restarts it
+    cmd = [sys.executable, "-c",
+           "import os, sys, runpy\n"
+           "if os.environ['DMLC_TASK_ID'] == '3' and not os.path.exists(%r):\n"
+           "    open(%r, 'w').write('x'); sys.exit(7)\n"
+           "sys.argv = [%r]; runpy.run_path(%r, run_name='__main__')\n"
+           % (str(flag), str(flag), worker, worker)]
+    job = SSHJob(cmd, hosts, 4, num_attempt=2, host_ip="127.0.0.1", tracker_port=9391,
+                 timeout=120, capture=True, print_fn=lambda m: None, ssh=[fake, "-o", "X=y"],
+                 workdir=str(tmp_path))
+    assert job.run() == 0, "".join("".join(o) for o in job.outputs)[-3000:]
+    out = "".join("".join(o) for o in job.outputs)
+    seen = sorted(re.findall(r"SSHW rank=(\d) host=(\w+) local=(\d)/(\d)", out))
+    assert seen == [("0", "nodeA", "0", "2"), ("1", "nodeA", "1", "2"), ("2", "nodeB", "0", "2"),
+                    ("3", "nodeB", "1", "2")], out[-3000:]
+    assert job.attempts == [1, 1, 1, 2]
