@@ -16,6 +16,15 @@ which the device plane picks its GPU (one process per GPU).  The tracker listens
 by default this host's address.
 
     python -m rabit_amd.launcher --cluster ssh --host-file hosts -n 16 -- python train.py
+
+Under an MPI launcher or Slurm (`--cluster mpi` / `--cluster slurm`) the job's processes belong
+to `mpirun` / `srun`: the launcher runs the tracker and one `mpirun -n N` (or `srun -n N`) of a
+small worker shim, which maps the scheduler's rank variables (OMPI_COMM_WORLD_RANK, PMI_RANK,
+PMIX_RANK, SLURM_PROCID and their local-rank counterparts) to DMLC_TASK_ID and LOCAL_RANK and
+runs the command as its child.  As with dmlc-submit's mpi mode, restarts are the scheduler's
+business there, not the launcher's.
+
+    python -m rabit_amd.launcher --cluster mpi -n 16 --mpi-args "--hostfile hosts" -- ./prog
 """
 from __future__ import annotations
 
@@ -214,6 +223,75 @@ class SSHJob(LocalJob):
             text=self.capture)
 
 
+_RANK_VARS = ("OMPI_COMM_WORLD_RANK", "PMIX_RANK", "PMI_RANK", "SLURM_PROCID")
+_LOCAL_RANK_VARS = ("OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID")
+_LOCAL_SIZE_VARS = ("OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE")
+
+
+def _first(env: Dict[str, str], names: Sequence[str]) -> Optional[str]:
+    for k in names:
+        if env.get(k, "") != "":
+            return env[k]
+    return None
+
+
+def shim_env(env: Dict[str, str], tracker: str, port: int, world: int) -> Dict[str, str]:
+    """the rabit worker environment of a process started by mpirun / srun"""
+    task = _first(env, _RANK_VARS)
+    if task is None:
+        raise RuntimeError("no MPI/Slurm rank variable (%s) in the environment"
+                           % ", ".join(_RANK_VARS))
+    out = dict(env)
+    out.update({"DMLC_TRACKER_URI": tracker, "DMLC_TRACKER_PORT": str(port),
+                "DMLC_TASK_ID": task, "DMLC_ROLE": "worker",
+                "DMLC_NUM_ATTEMPT": env.get("DMLC_NUM_ATTEMPT", "0"),
+                "DMLC_NUM_WORKER": str(world), "rabit_world_size": str(world)})
+    local = _first(env, _LOCAL_RANK_VARS)
+    if local is not None and "LOCAL_RANK" not in env:
+        out["LOCAL_RANK"] = local
+    size = _first(env, _LOCAL_SIZE_VARS)
+    if size is not None and "LOCAL_WORLD_SIZE" not in env:
+        out["LOCAL_WORLD_SIZE"] = size.split("(")[0]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return out
+
+
+def run_shim(argv: Sequence[str]) -> int:
+    """worker side of --cluster mpi|slurm: `--shim URI PORT WORLD -- cmd...`"""
+    tracker, port, world = argv[0], int(argv[1]), int(argv[2])
+    cmd = list(argv[3:])
+    if cmd and cmd[0] == "--":
+        cmd = cmd[1:]
+    return subprocess.call(cmd, env=shim_env(dict(os.environ), tracker, port, world))
+
+
+class SchedulerJob:
+    """A rabit job whose processes are started by mpirun or srun (see the module docstring)"""
+
+    def __init__(self, cmd: Sequence[str], num_workers: int, launcher: Sequence[str],
+                 host_ip: Optional[str] = None, tracker_port: int = 9091,
+                 timeout: Optional[float] = None, print_fn=None):
+        self.cmd = list(cmd)
+        self.n = num_workers
+        self.launcher = list(launcher)
+        self.timeout = timeout
+        self.tracker = RabitTracker(host_ip or default_host_ip(), num_workers, tracker_port,
+                                    print_fn=print_fn)
+
+    def command(self) -> List[str]:
+        return self.launcher + [sys.executable, "-m", "rabit_amd.launcher", "--shim",
+                                self.tracker.host_ip, str(self.tracker.port), str(self.n),
+                                "--"] + self.cmd
+
+    def run(self) -> int:
+        self.tracker.start(self.n)
+        rc = subprocess.call(self.command(), timeout=self.timeout)
+        if rc == 0:
+            self.tracker.join(30)
+        return rc
+
+
 def default_host_ip() -> str:
     """an address of this host other peers can reach (the tracker binds and advertises it)"""
     try:
@@ -225,11 +303,17 @@ def default_host_ip() -> str:
 
 
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="launch an xrabit job (local or over ssh)")
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] == "--shim":
+        sys.exit(run_shim(argv[1:]))
+    ap = argparse.ArgumentParser(description="launch an xrabit job (local, ssh, mpi or slurm)")
     ap.add_argument("-n", "--num-workers", type=int, required=True)
     ap.add_argument("--num-attempt", "--local-num-attempt", type=int, default=1,
                     help="restarts allowed per worker (fault-tolerance tests)")
-    ap.add_argument("--cluster", choices=["local", "ssh"], default="local")
+    ap.add_argument("--cluster", choices=["local", "ssh", "mpi", "slurm"], default="local")
+    ap.add_argument("--mpi-args", default="", help="--cluster mpi: extra mpirun arguments")
+    ap.add_argument("--mpirun", default="mpirun", help="--cluster mpi: the MPI launcher")
+    ap.add_argument("--srun", default="srun", help="--cluster slurm: the Slurm launcher")
     ap.add_argument("--host-file", help="--cluster ssh: host[:slots] per line")
     ap.add_argument("--ssh", default="ssh -o StrictHostKeyChecking=no -o BatchMode=yes",
                     help="--cluster ssh: the ssh command (host and remote command appended)")
@@ -246,6 +330,14 @@ def main(argv=None):
     if not cmd:
         ap.error("missing worker command")
     env = dict(kv.split("=", 1) for kv in args.env)
+    if args.cluster in ("mpi", "slurm"):
+        if args.cluster == "mpi":
+            launcher = shlex.split(args.mpirun) + ["-n", str(args.num_workers)] + \
+                shlex.split(args.mpi_args)
+        else:
+            launcher = shlex.split(args.srun) + ["-n", str(args.num_workers)]
+        job = SchedulerJob(cmd, args.num_workers, launcher, args.host_ip, args.port, args.timeout)
+        sys.exit(job.run())
     if args.cluster == "ssh":
         if not args.host_file:
             ap.error("--cluster ssh needs --host-file")

@@ -144,6 +144,7 @@ def test_bench_torchrun_shared_gpu(n):
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["transport"]["direct"] == 1, rec
     assert rec["result_check"], rec
+    assert "post_headline_failure" not in rec, rec["post_headline_failure"]
     # every available transport x input variant ran and matched the host fp64 reference
     ran = [v for v in rec["variants"] if v["available"]]
     assert {(v["transport"], v["input"]) for v in ran} >= {

@@ -138,3 +138,30 @@ def test_launcher_ssh_cluster(tmp_path):
     assert seen == [("0", "nodeA", "0", "2"), ("1", "nodeA", "1", "2"), ("2", "nodeB", "0", "2"),
                     ("3", "nodeB", "1", "2")], out[-3000:]
     assert job.attempts == [1, 1, 1, 2]
+
+
+def test_launcher_mpi_cluster(tmp_path):
+    """--cluster mpi: one mpirun of the worker shim, which maps the MPI rank variables to the
+    rabit worker environment (task id, LOCAL_RANK per node) and runs the command."""
+    fake = os.path.join(ROOT, "tests", "scripts", "fake_mpirun.sh")
+    worker = os.path.join(ROOT, "tests", "scripts", "ssh_worker.py")
+    out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "--cluster", "mpi",
+                          "--mpirun", fake, "--host-ip", "127.0.0.1", "--port", "9411", "-n", "4",
+                          "--timeout", "120", "--", sys.executable, worker],
+                         capture_output=True, text=True, timeout=180, cwd=str(tmp_path),
+                         env=dict(os.environ, PYTHONPATH=ROOT))
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    seen = sorted(re.findall(r"SSHW rank=(\d) host=\w+ local=(\d)/(\d)", out.stdout))
+    assert seen == [("0", "0", "2"), ("1", "1", "2"), ("2", "0", "2"), ("3", "1", "2")], out.stdout
+
+
+def test_shim_env_schedulers():
+    from rabit_amd.launcher import shim_env
+    e = shim_env({"SLURM_PROCID": "5", "SLURM_LOCALID": "1", "SLURM_NTASKS_PER_NODE": "8(x2)"},
+                 "10.0.0.1", 9091, 16)
+    assert (e["DMLC_TASK_ID"], e["LOCAL_RANK"], e["LOCAL_WORLD_SIZE"]) == ("5", "1", "8")
+    assert e["DMLC_TRACKER_URI"] == "10.0.0.1" and e["rabit_world_size"] == "16"
+    e = shim_env({"PMI_RANK": "2", "MPI_LOCALRANKID": "0", "LOCAL_RANK": "3"}, "h", 1, 4)
+    assert e["DMLC_TASK_ID"] == "2" and e["LOCAL_RANK"] == "3"  # an explicit LOCAL_RANK wins
+    with pytest.raises(RuntimeError):
+        shim_env({}, "h", 1, 4)
