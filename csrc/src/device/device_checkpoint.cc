@@ -23,6 +23,16 @@ DeviceCheckpoint::DeviceCheckpoint(DevicePlane *plane) : plane_(plane) {
   loader_.owner = this;
 }
 
+void DeviceCheckpoint::set_mirror_low_priority(bool low) {
+  if (!low) return;
+  int least = 0, greatest = 0;
+  CheckHip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+  CheckHip(hipStreamSynchronize(side_), "hipStreamSynchronize(ckpt)");
+  CheckHip(hipStreamDestroy(side_), "hipStreamDestroy(ckpt)");
+  CheckHip(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, least),
+           "hipStreamCreateWithPriority(ckpt)");
+}
+
 DeviceCheckpoint::~DeviceCheckpoint() {
   (void)hipStreamSynchronize(side_);
   for (auto &h : half_) {
@@ -109,7 +119,10 @@ void DeviceCheckpoint::Half::StartMirror() const {
   size_t off = 0;
   for (size_t i = 0; i < sizes.size(); ++i) {
     if (sizes[i] != 0) {
-      CheckHip(hipMemcpyAsync(o->pinned_ + off, dev[i], sizes[i], hipMemcpyDeviceToHost, o->side_),
+      CheckHip(o->mirror_ctas_ > 0
+                   ? LaunchCopyNarrow(o->pinned_ + off, dev[i], sizes[i], o->mirror_ctas_, o->side_)
+                   : hipMemcpyAsync(o->pinned_ + off, dev[i], sizes[i], hipMemcpyDeviceToHost,
+                                    o->side_),
                "D2H mirror");
     }
     off += sizes[i];

@@ -65,6 +65,10 @@ class DeviceCheckpoint {
   /*! \brief mirror policy */
   enum MirrorMode { kMirrorIdle = 0, kMirrorAlways = 1, kMirrorOff = 2 };
   void set_mirror_mode(int m) { mirror_mode_ = m; }
+  /*! \brief workgroups of the narrow D2H copy kernel of the host mirror; 0: hipMemcpyAsync */
+  void set_mirror_ctas(int c) { mirror_ctas_ = c; }
+  /*! \brief run the mirrors on a stream of the lowest priority (before the first snapshot) */
+  void set_mirror_low_priority(bool low);
   /*! \brief snapshot slots: 2, 3, or 0 = by size (3 below three_slot_max bytes) */
   void set_slots(int n, size_t three_slot_max) {
     slots_req_ = n;
@@ -121,6 +125,7 @@ class DeviceCheckpoint {
   size_t three_slot_max_{size_t(4) << 30};
   int cur_{-1};
   int mirror_mode_{kMirrorIdle};
+  int mirror_ctas_{0};
   char *pinned_{nullptr};  // the host mirror, shared by the slots
   size_t pinned_cap_{0};
   const Half *pinned_owner_{nullptr};

@@ -54,6 +54,11 @@ hipError_t LaunchChecksum(const void *buf, size_t nbytes, unsigned long long *ou
 /*! \brief device-to-device copy: 16-byte-per-lane kernel for the aligned bulk (the blit
  *  kernel behind hipMemcpyAsync D2D streams slower), hipMemcpyAsync for an unaligned rest */
 hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stream);
+/*! \brief copy with `ctas` grid-stride workgroups (device -> pinned host mirrors: PCIe-bound,
+ *  so a few workgroups suffice and the other CUs stay with the caller's work); dst may be
+ *  device-accessible host memory */
+hipError_t LaunchCopyNarrow(void *dst, const void *src, size_t bytes, int ctas,
+                            hipStream_t stream);
 /*!
  * \brief fault injection (mock_dev_hang): a one-wave kernel that models a wedged kernel on the
  *        stream.  It ignores the engine's abort word; it ends when the host sets *release or

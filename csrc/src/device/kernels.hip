@@ -322,6 +322,32 @@ __global__ __launch_bounds__(kBlock) void CopyTileKernel(uint4 *__restrict__ dst
   }
 }
 
+/*!
+ * Narrow copy for device -> pinned host memory (rabit_device_mirror_ctas > 0 for checkpoint
+ * mirrors): `ctas` workgroups walk the buffer grid-stride, 4 x 16 B per lane in flight, with
+ * nontemporal stores.  PCIe (~55 GB/s) bounds the copy, so a few workgroups reach it.  It is NOT
+ * the default: hipMemcpyAsync D2H runs a blit kernel with one 512-lane workgroup on every CU,
+ * and measured against 20 bf16 8192^3 GEMMs on the caller's stream (tools/mirror_probe.py,
+ * profiles/r2_s15_mirror) the blit hides ~55 % of a 256 MiB mirror (16.6 -> 18.8 ms) while
+ * this kernel at 4-1024 workgroups hides none (21.4-23.3 ms): a few CUs slowed for the whole
+ * copy stretch the GEMM's last wave of tiles.
+ */
+__global__ __launch_bounds__(kBlock) void CopyNarrowKernel(uint4 *__restrict__ dst,
+                                                          const uint4 *__restrict__ src,
+                                                          size_t nvec) {
+  constexpr int U = 4;
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + (U - 1) * stride < nvec; i += U * stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) StoreNT(&dst[i + u * stride], v[u]);
+  }
+  for (; i < nvec; i += stride) StoreNT(&dst[i], src[i]);
+}
+
 // ---------------------------------------------------------------- checksum
 /*!
  * Position-weighted checksum over 16-byte vectors v (words w0..w3):
@@ -547,6 +573,27 @@ hipError_t LaunchCopy(void *dst, const void *src, size_t bytes, hipStream_t stre
   if (done < bytes) {
     return hipMemcpyAsync(static_cast<char *>(dst) + done, static_cast<const char *>(src) + done,
                           bytes - done, hipMemcpyDeviceToDevice, stream);
+  }
+  return hipSuccess;
+}
+
+hipError_t LaunchCopyNarrow(void *dst, const void *src, size_t bytes, int ctas,
+                            hipStream_t stream) {
+  if (bytes == 0 || dst == src) return hipSuccess;
+  const size_t nvec = Aligned16(dst) && Aligned16(src) ? bytes / 16 : 0;
+  if (nvec != 0) {
+    const size_t per = static_cast<size_t>(kBlock) * 4;
+    const unsigned grid = static_cast<unsigned>(
+        std::max<size_t>(1, std::min<size_t>(std::max(ctas, 1), (nvec + per - 1) / per)));
+    hipLaunchKernelGGL(CopyNarrowKernel, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<uint4 *>(dst), static_cast<const uint4 *>(src), nvec);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const size_t done = nvec * 16;
+  if (done < bytes) {
+    return hipMemcpyAsync(static_cast<char *>(dst) + done, static_cast<const char *>(src) + done,
+                          bytes - done, hipMemcpyDefault, stream);
   }
   return hipSuccess;
 }

@@ -145,6 +145,16 @@ void EngineBase::SetParam(const char *name, const char *val) {
       utils::Error("rabit_device_ckpt_mirror must be always, idle or off (got %s)", val);
     }
   }
+  if (is("rabit_device_mirror_priority")) {
+    utils::Check(!strcmp(val, "low") || !strcmp(val, "normal"),
+                 "rabit_device_mirror_priority must be low or normal (got %s)", val);
+    mirror_low_prio_ = !strcmp(val, "low");
+  }
+  if (is("rabit_device_mirror_ctas")) {
+    mirror_ctas_ = atoi(val);
+    utils::Check(mirror_ctas_ >= 0 && mirror_ctas_ <= 4096,
+                 "rabit_device_mirror_ctas must be 0 (hipMemcpyAsync) or 1..4096");
+  }
   if (is("rabit_device_ckpt_slots")) {
     ckpt_slots_ = atoi(val);
     utils::Check(ckpt_slots_ == 0 || ckpt_slots_ == 2 || ckpt_slots_ == 3,
@@ -628,6 +638,8 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
+    dev_ckpt_->set_mirror_ctas(mirror_ctas_);
+    dev_ckpt_->set_mirror_low_priority(mirror_low_prio_);
     dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
   trace::Scope ts("device_snapshot", rank_, version_number_, seq_counter_, 0, 1);
@@ -648,6 +660,8 @@ int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
+    dev_ckpt_->set_mirror_ctas(mirror_ctas_);
+    dev_ckpt_->set_mirror_low_priority(mirror_low_prio_);
     dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
   dev_local_.owner = this;

@@ -234,6 +234,8 @@ class EngineBase : public IEngine {
   bool shm_enabled_{true};          // rabit_host_shm
   int ckpt_mirror_mode_{0};          // rabit_device_ckpt_mirror: 0 idle, 1 always, 2 off
   int ckpt_slots_{0};                // rabit_device_ckpt_slots: 2, 3, 0 = by size
+  bool mirror_low_prio_{false};      // rabit_device_mirror_priority=low
+  int mirror_ctas_{0};               // rabit_device_mirror_ctas: D2H mirror kernel width (0: hipMemcpyAsync)
   size_t ckpt_3slot_max_{size_t(4) << 30};  // by size: 3 slots below this many bytes
   size_t shm_min_{1u << 20};        // rabit_host_shm_min
   size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)

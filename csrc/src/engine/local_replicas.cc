@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "device/device_plane.h"
+#include "device/kernels.h"
 #include "rabit/internal/utils.h"
 
 namespace rabit {
@@ -113,7 +114,11 @@ void LocalReplicas::Mirror(int v, hipStream_t stream) {
   }
   device::CheckHip(hipEventRecord(ready_, stream), "hipEventRecord");
   device::CheckHip(hipStreamWaitEvent(side_, ready_, 0), "hipStreamWaitEvent");
-  device::CheckHip(hipMemcpyAsync(pinned_, slots_[v][0].dev, bytes, hipMemcpyDeviceToHost, side_),
+  device::CheckHip(mirror_ctas_ > 0
+                       ? device::LaunchCopyNarrow(pinned_, slots_[v][0].dev, bytes, mirror_ctas_,
+                                                  side_)
+                       : hipMemcpyAsync(pinned_, slots_[v][0].dev, bytes, hipMemcpyDeviceToHost,
+                                        side_),
                    "D2H local mirror");
   device::CheckHip(hipEventRecord(done_, side_), "hipEventRecord");
   mirror_pending_ = true;

@@ -74,6 +74,8 @@ class LocalReplicas {
   void BeforeWrite(int v, hipStream_t stream);
   uint64_t mirrors() const { return mirrors_; }
   uint64_t mirrors_skipped() const { return mirrors_skipped_; }
+  /*! \brief workgroups of the narrow D2H copy kernel of the mirror; 0: hipMemcpyAsync */
+  void set_mirror_ctas(int c) { mirror_ctas_ = c; }
 
  private:
   struct Slot {
@@ -95,6 +97,7 @@ class LocalReplicas {
   void *pinned_{nullptr};
   size_t pinned_cap_{0};
   bool mirror_pending_{false};
+  int mirror_ctas_{0};
   int mirror_version_{-1};
   uint64_t mirrors_{0}, mirrors_skipped_{0};
 };
