@@ -209,18 +209,34 @@ class SSHJob(LocalJob):
         return e
 
     def remote_command(self, task: int, attempt: int) -> str:
+        """The remote shell line: the worker runs in the background with stdin from /dev/null,
+        and a watcher reads the session's stdin (kept open by the launcher) until EOF, then
+        terminates the worker.  A killed launcher or a dropped connection therefore ends the
+        remote worker too, instead of leaving it behind on its host."""
         exports = " ".join("%s=%s" % (k, shlex.quote(v))
                            for k, v in sorted(self._remote_env(task, attempt).items()))
-        return "cd %s && env %s %s" % (shlex.quote(self.workdir), exports,
-                                       " ".join(shlex.quote(c) for c in self.cmd))
+        worker = "env %s %s" % (exports, " ".join(shlex.quote(c) for c in self.cmd))
+        return ("cd %s || exit 1; exec 3<&0; %s </dev/null & w=$!; "
+                "( cat <&3 >/dev/null 2>&1; kill -TERM $w 2>/dev/null ) >/dev/null 2>&1 & "
+                "exec 3<&-; wait $w" % (shlex.quote(self.workdir), worker))
 
     def _spawn(self, task: int, attempt: int) -> subprocess.Popen:
         host = self.placement[task][0]
         return subprocess.Popen(
             self.ssh + [host, self.remote_command(task, attempt)],
+            stdin=subprocess.PIPE,  # held open: its EOF tells the remote watcher to stop
             stdout=subprocess.PIPE if self.capture else None,
             stderr=subprocess.STDOUT if self.capture else None,
             text=self.capture)
+
+    def kill(self):
+        with self._lock:
+            self._stop = True
+            for p in self._procs:
+                if p is not None and p.poll() is None:
+                    if p.stdin is not None:
+                        p.stdin.close()
+                    p.kill()
 
 
 _RANK_VARS = ("OMPI_COMM_WORLD_RANK", "PMIX_RANK", "PMI_RANK", "SLURM_PROCID")

@@ -165,3 +165,45 @@ def test_shim_env_schedulers():
     assert e["DMLC_TASK_ID"] == "2" and e["LOCAL_RANK"] == "3"  # an explicit LOCAL_RANK wins
     with pytest.raises(RuntimeError):
         shim_env({}, "h", 1, 4)
+
+
+def test_launcher_ssh_kill_reaches_remote_worker(tmp_path):
+    """killing an ssh job ends the remote workers too: each remote shell watches its session's
+    stdin, which the launcher holds open, and terminates its worker on EOF"""
+    import time
+    from rabit_amd.launcher import SSHJob
+
+    fake = os.path.join(ROOT, "tests", "scripts", "fake_ssh.sh")
+    pidfile = tmp_path / "pids"
+    cmd = [sys.executable, "-c",
+           "import os, time\n"
+           "open(%r, 'a').write('%%d\\n' %% os.getpid())\n"
+           "time.sleep(300)\n" % str(pidfile)]
+    job = SSHJob(cmd, [("nodeA", 2)], 2, host_ip="127.0.0.1", tracker_port=9421,
+                 ssh=[fake], workdir=str(tmp_path), print_fn=lambda m: None)
+    job.tracker.start(2)
+    import threading
+    threads = [threading.Thread(target=job._run_worker, args=(i,), daemon=True) for i in range(2)]
+    for t in threads:
+        t.start()
+    deadline = time.time() + 30
+    while time.time() < deadline and (not pidfile.exists() or
+                                      len(pidfile.read_text().split()) < 2):
+        time.sleep(0.1)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 2
+    job.kill()
+
+    def alive(pid):
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        # a zombie (exited, not yet reaped by its shell) counts as gone
+        with open("/proc/%d/stat" % pid) as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+
+    deadline = time.time() + 15
+    while time.time() < deadline and any(alive(p) for p in pids):
+        time.sleep(0.1)
+    assert not any(alive(p) for p in pids), "remote workers survived the launcher's kill"
