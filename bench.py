@@ -390,7 +390,16 @@ def main():
     # the robust engine logs every result until the next checkpoint: reserve the HBM log for
     # the check, warmup and timed steps up front (one allocation), as a job would size it for
     # the results of one iteration, so the timed loop never waits on hipMalloc
-    log = {"rabit_device_log_reserve": str((args.warmup + args.steps + 3) * n * 4)}
+    # Long runs (large --steps) log more than the default 64 GiB HBM cap: let the log use this
+    # rank's share of the free HBM (less 16 GiB for the heap, stages and the extras' buffers)
+    # before it spills to pinned host memory, and never reserve more than that share.
+    free_hbm = torch.cuda.mem_get_info(gpu)[0]
+    ranks_here = max(1, -(-int(os.environ.get("LOCAL_WORLD_SIZE", world)) // ngpu))
+    share = max(1 << 30, free_hbm // ranks_here - (16 << 30))
+    want = (args.warmup + args.steps + 3) * n * 4
+    log = {"rabit_device_log_reserve": str(min(want, share))}
+    if want > (64 << 30):
+        log["rabit_device_log_cap"] = str(max(64 << 30, share))
     ctx = init_from_env(lib="standard" if args.engine == "robust" else "base",
                         rabit_world1_fastpath=0, rabit_device=gpu, **heap, **tune, **log)
     dev = torch.device("cuda", gpu)

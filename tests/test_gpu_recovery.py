@@ -56,3 +56,22 @@ def test_device_checkpoint_recovery_two_slots(replay):
     # two slots of (64 Ki floats + 7 doubles) each, 256-byte rounded
     hbm = [int(x) for x in re.findall(r"hbm=(\d+)", out)]
     assert max(hbm) <= 2 * ((1 << 18) + 256), hbm
+
+
+@pytest.mark.parametrize("ctas", ["8", "0"])
+def test_device_checkpoint_mirror_copy_engines(ctas):
+    """the pinned host mirror written by the narrow copy kernel (rabit_device_mirror_ctas=8) or
+    by hipMemcpyAsync (0) is what a restarted rank gets over TCP (replay=0, every checkpoint
+    mirrored): its model must come back exactly"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    script = os.path.join(ROOT, "tests", "scripts", "device_ckpt_recover.py")
+    job = LocalJob([sys.executable, script, "mock=0,1,0,0", "mock=2,3,1,0",
+                    "rabit_device_ckpt_mirror=always", "rabit_device_mirror_ctas=" + ctas,
+                    "rabit_device_mirror_priority=low", "rabit_device_replay=0"], 3, 4,
+                   capture=True, timeout=240, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-4000:]
+    assert out.count("DEVCKPT OK") == 3, out[-3000:]
+    assert "reloaded version" in out
