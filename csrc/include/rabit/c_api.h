@@ -115,6 +115,16 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode);
  */
 RABIT_DLL int RabitDevSetFused(int fused);
 /*!
+ * \brief xrabit extension: in-place RCCL allreduce of a device buffer, enqueued on hip_stream
+ *        with no host-side synchronisation, so it can be captured into a hipGraph together with
+ *        the step's kernels.  Non-fault-tolerant engines only (base / empty): the op has no
+ *        sequence number, result log or replay.
+ * \return 0; -1 no device plane, -2 no RCCL communicator, -3 dtype/op RCCL lacks (BitOR),
+ *         -4 fault-tolerant engine, -5 RCCL refused the call (RabitGetLastError says which)
+ */
+RABIT_DLL int RabitDevGraphAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
+                                     void *hip_stream);
+/*!
  * \brief xrabit extension: per-phase hipEvent timing of the direct transport's classic two-shot
  *        allreduce (stage, barrier, reduce, barrier, gather) from now on, with fresh totals
  *        (on = 1), or off (0); averages appear in RabitGetStats as direct_phase_us.

@@ -283,6 +283,28 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode) {
   return 0;
 }
 
+RABIT_DLL int RabitDevGraphAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
+                                     void *hip_stream) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) {
+    g_last_error = "graph allreduce needs the device plane";
+    return -1;
+  }
+  const char *name = e->EngineName();
+  if (!std::strcmp(name, "robust") || !std::strcmp(name, "mock")) {
+    // no sequence number, result log or replay: a captured collective cannot be recovered
+    g_last_error = "graph allreduce bypasses fault tolerance: use the base engine (lib='base')";
+    return -4;
+  }
+  std::string why;
+  const int r = Guard([&]() {
+    return e->DevGraphAllreduce(buf, count, enum_dtype, enum_op,
+                                static_cast<hipStream_t>(hip_stream), &why);
+  }, -1);
+  if (r != 0 && !why.empty()) g_last_error = why;
+  return r;
+}
+
 RABIT_DLL int RabitDevSetFused(int fused) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
   if (e == nullptr || e->device_plane() == nullptr || !e->device_plane()->has_peers()) return -1;

@@ -655,6 +655,16 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   return Status::kSuccess;
 }
 
+int DevicePlane::GraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream) {
+  if (comm_ == nullptr) return -2;
+  ncclDataType_t t;
+  ncclRedOp_t o;
+  if (!RcclType(dtype, &t) || !RcclOp(op, &o)) return -3;
+  if (count == 0) return 0;
+  DeviceGuard dg(device_);
+  return ncclAllReduce(buf, buf, count, t, o, comm_, stream) == ncclSuccess ? 0 : -5;
+}
+
 Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                                     size_t type_nbytes, DeviceReduceLauncher *launcher,
                                     const FailureProbe &probe) {

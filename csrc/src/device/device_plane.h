@@ -278,6 +278,13 @@ class DevicePlane {
    *        recv.  prep is a PrepOp (kPrepCopy: none).  recv2 is written only when the op
    *        succeeds on this rank, so a retry still finds the input.
    */
+  /*!
+   * \brief in-place RCCL allreduce enqueued on `stream` and nothing else: no host wait, no
+   *        event, no result log, so it may be captured into a hipGraph.  Outside fault
+   *        tolerance (non-robust engines only).  0 on success, -2 without a communicator, -3
+   *        for a dtype/op RCCL lacks (BitOR), -5 when RCCL refuses the call.
+   */
+  int GraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream);
   Status Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
                    int prep, double alpha, const FailureProbe &probe);
   /*! \brief launcher of a user device reduction (IEngine::DeviceReduceLauncher) */

@@ -620,6 +620,32 @@ void FoldIntoLocal(int *n, void *const **ptrs, const size_t **nbytes, int *nl,
 }
 }  // namespace
 
+int EngineBase::DevGraphAllreduce(void *buf, size_t count, int dtype, int op,
+                                  hipStream_t stream, std::string *why) {
+  if (dev_ == nullptr) {
+    *why = "graph allreduce needs the device plane";
+    return -1;
+  }
+  if (GetWorldSize() == 1 && !world1_transport_) return 0;  // a one-rank reduction is identity
+  device::DeviceGuard dg(dev_->device());
+  if (!dev_->has_comm()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+      *why = "graph allreduce: make one eager call before capturing (it brings RCCL up)";
+      return -2;
+    }
+    if (EnsureDeviceComm() != Status::kSuccess || !dev_->has_comm()) {
+      *why = "graph allreduce needs an RCCL communicator";
+      return -2;
+    }
+  }
+  const int r = dev_->GraphAllreduce(buf, count, dtype, op, stream);
+  if (r == -3) *why = "graph allreduce: dtype/op not supported by RCCL";
+  if (r == -5) *why = "graph allreduce: ncclAllReduce failed";
+  if (r == 0) stats_.n_device_ops += 1;
+  return r;
+}
+
 void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                const std::string &meta, int nl, void *const *lptrs,
                                const size_t *lnbytes) {

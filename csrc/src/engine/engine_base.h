@@ -98,6 +98,13 @@ class EngineBase : public IEngine {
                                     int prep, double alpha, const char *_file, const int _line,
                                     const char *_caller);
   /*!
+   * \brief capturable in-place RCCL allreduce (RabitDevGraphAllreduce): brings the device
+   *        communicator up on first use (a collective: make the first call eagerly, on every
+   *        rank), then only enqueues ncclAllReduce on `stream`.  0 or a negative code (c_api.h)
+   */
+  int DevGraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream,
+                        std::string *why);
+  /*!
    * \brief checkpoint HBM buffers: HBM snapshot + async pinned mirror, registered as a lazy
    *        global checkpoint (see device/device_checkpoint.h).  nl > 0: lptrs are this rank's
    *        local model (per-rank state): the robust engine keeps it, and the replicas of its

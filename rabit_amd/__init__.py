@@ -14,7 +14,8 @@ from .core import (BITOR, DTYPE_ENUM, DTYPE_ENUM__, MAX, MIN, PREP_ABS, PREP_COP
                    is_distributed, last_error, lazy_checkpoint, lib, load_checkpoint,
                    set_error_mode, stats, tracker_print, version_number, dump_trace,
                    checkpoint_tensors, load_checkpoint_tensors, symmetric_empty,
-                   set_device_transport, set_phase_timing, TRANSPORT_AUTO, TRANSPORT_DIRECT,
+                   set_device_transport, set_phase_timing, allreduce_graphable, TRANSPORT_AUTO,
+                   TRANSPORT_DIRECT,
                    TRANSPORT_RCCL)
 
 __version__ = "0.1.0"

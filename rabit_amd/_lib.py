@@ -86,6 +86,7 @@ def _declare(d: ctypes.CDLL) -> None:
                                              ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
         "RabitDevSetTransport": (c_int, [c_int, c_int]),
         "RabitDevSetFused": (c_int, [c_int]),
+        "RabitDevGraphAllreduce": (c_int, [c_void_p, c_size_t, c_int, c_int, c_void_p]),
         "RabitDevSetPhaseTiming": (c_int, [c_int]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),

@@ -448,6 +448,25 @@ def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str]
     return True
 
 
+def allreduce_graphable(t, op: int):
+    """In-place RCCL allreduce of an HBM tensor on the current stream, with no host-side
+    synchronisation: unlike allreduce(), it can be captured into a hipGraph with the rest of
+    the step (torch.cuda.graph / rabit_amd.parallel.GraphedStep).  Non-fault-tolerant engines
+    only (init(lib="base")): the op has no sequence number, result log or replay.  Identity at
+    world size 1 without a communicator."""
+    import torch
+
+    _check_init()
+    if not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
+        raise TypeError("allreduce_graphable takes a contiguous HBM (cuda) tensor")
+    stream = torch.cuda.current_stream(t.device).cuda_stream
+    r = _LIB.RabitDevGraphAllreduce(t.data_ptr(), t.numel(), _torch_dtype_enum(t), int(op),
+                                    stream)
+    if r != 0:
+        raise RuntimeError("allreduce_graphable: %s" % last_error())
+    return t
+
+
 def set_phase_timing(on: bool) -> bool:
     """Time the phases of the direct transport's classic two-shot allreduce (stage, barrier,
     reduce, barrier, gather) with hipEvents from now on, with fresh totals (on=True), or stop.

@@ -1,0 +1,63 @@
+"""allreduce_graphable inside a captured hipGraph (base engine, one GPU): the world-1 transport
+hook gives the rank a one-rank RCCL communicator, so the captured step holds a real
+ncclAllReduce node between the step's kernels.  Replays must give the eager result every time;
+the fault-tolerant engines and BitOR must be refused.  argv[1]: base | standard."""
+import sys
+
+import torch
+
+import rabit_amd as rabit
+
+lib = sys.argv[1]
+rabit.init(sys.argv[2:], lib=lib, rabit_device=0, rabit_world1_fastpath=0,
+           rabit_device_world1_transport=1, rabit_device_algo="rccl")
+dev = torch.device("cuda", 0)
+x = torch.arange(1 << 20, device=dev, dtype=torch.float32).remainder_(113)
+if lib != "base":
+    try:
+        rabit.allreduce_graphable(x, rabit.SUM)
+    except RuntimeError as e:
+        assert "fault tolerance" in str(e), e
+        print("GRAPHAR REFUSED", flush=True)
+    rabit.finalize()
+    sys.exit(0)
+try:
+    rabit.allreduce_graphable(torch.zeros(8, device=dev, dtype=torch.int32), rabit.BITOR)
+    raise AssertionError("BitOR accepted")
+except RuntimeError as e:
+    assert "not supported" in str(e), e
+
+y = torch.empty_like(x)
+z = torch.empty_like(x)
+side = torch.cuda.Stream()
+
+
+def step():
+    torch.mul(x, 2.0, out=y)
+    rabit.allreduce_graphable(y, rabit.SUM)
+    torch.add(y, 1.0, out=z)
+    for dt in (torch.bfloat16, torch.float16):  # extended dtypes ride through RCCL too
+        h = y.to(dt)
+        rabit.allreduce_graphable(h, rabit.MAX)
+        z.add_(h.float()).sub_(y)
+
+
+side.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(side):
+    for _ in range(2):
+        step()
+torch.cuda.current_stream().wait_stream(side)
+want = x * 2.0 + 1.0
+torch.cuda.synchronize()
+assert torch.equal(z, want), "eager"
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    step()
+for i in range(4):
+    x.add_(1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(z, x * 2.0 + 1.0), ("replay", i)
+assert rabit.stats()["device_rccl"] == 1, "no RCCL communicator: nothing was captured"
+print("GRAPHAR OK", flush=True)
+rabit.finalize()

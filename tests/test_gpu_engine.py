@@ -128,3 +128,18 @@ def test_transports_world1(algo, extra):
     out = "".join("".join(o) for o in job.outputs)
     assert rc == 0, out[-5000:]
     assert "TRANSPORT1 OK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("lib", ["base", "standard"])
+def test_allreduce_graphable(lib):
+    """allreduce_graphable: an ncclAllReduce captured into a hipGraph with the step's kernels
+    replays exactly (base engine); the fault-tolerant engine refuses it"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rabit_amd.launcher import LocalJob
+    job = LocalJob([sys.executable, os.path.join(ROOT, "tests", "scripts", "graph_allreduce.py"),
+                    lib], 1, 1, capture=True, timeout=240, print_fn=lambda m: None)
+    rc = job.run()
+    out = "".join("".join(o) for o in job.outputs)
+    assert rc == 0, out[-5000:]
+    assert ("GRAPHAR OK" if lib == "base" else "GRAPHAR REFUSED") in out, out[-3000:]
