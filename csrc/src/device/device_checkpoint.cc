@@ -33,7 +33,40 @@ void DeviceCheckpoint::set_mirror_low_priority(bool low) {
            "hipStreamCreateWithPriority(ckpt)");
 }
 
+void DeviceCheckpoint::set_mirror_engine(int engine, int ctas) {
+  mirror_engine_ = engine;
+  if (ctas > 0) mirror_ctas_ = ctas;
+  dma_.reset();
+  if (engine == kEngineSdma) {
+    std::unique_ptr<DmaCopier> d(new DmaCopier(plane_->device()));
+    if (d->ok()) {
+      dma_ = std::move(d);
+    } else {
+      utils::HandleLogInfo("[xrabit] SDMA mirror unavailable (%s): using hipMemcpyAsync\n",
+                           d->why().c_str());
+      mirror_engine_ = kEngineHip;
+    }
+  }
+}
+
+bool DeviceCheckpoint::MirrorDone(const Half &h) const {
+  if (dma_) return dma_->Done(h.ticket);
+  const hipError_t q = hipEventQuery(h.d2h_done);
+  if (q != hipErrorNotReady) CheckHip(q, "checkpoint mirror query");
+  return q == hipSuccess;
+}
+
+void DeviceCheckpoint::WaitMirror(const Half &h) const {
+  if (dma_) {
+    dma_->Wait(h.ticket);
+    return;
+  }
+  CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
+}
+
 DeviceCheckpoint::~DeviceCheckpoint() {
+  if (dma_) dma_->WaitAll();
+  dma_.reset();
   (void)hipStreamSynchronize(side_);
   for (auto &h : half_) {
     for (void *p : h.dev) (void)hipFree(p);
@@ -64,7 +97,7 @@ const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const s
   cur_ = (cur_ + 1) % nslots_;
   Half &h = half_[cur_];
   // a mirror still reading this slot must finish before its buffers are reused
-  CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
+  WaitMirror(h);
   if (pinned_owner_ == &h) pinned_owner_ = nullptr;  // its bytes are about to change
   h.dev.resize(n, nullptr);
   h.cap.resize(n, 0);
@@ -84,12 +117,7 @@ const Serializable *DeviceCheckpoint::Snapshot(int n, void *const *ptrs, const s
   // the caller may overwrite its tensors only after the snapshot read them
   plane_->Finish(FailureProbe(), false);
   // 2. pinned host mirror on the side stream: always, or when the previous one is done
-  bool idle = last_mirror_ == nullptr;
-  if (!idle) {
-    const hipError_t q = hipEventQuery(last_mirror_->d2h_done);
-    if (q != hipErrorNotReady) CheckHip(q, "checkpoint mirror query");
-    idle = q == hipSuccess;
-  }
+  const bool idle = last_mirror_ == nullptr || MirrorDone(*last_mirror_);
   if (mirror_mode_ == kMirrorAlways || (mirror_mode_ == kMirrorIdle && idle)) {
     h.StartMirror();
     mirrors_ += 1;
@@ -104,7 +132,8 @@ void DeviceCheckpoint::Half::StartMirror() const {
   size_t total = 0;
   for (size_t s : sizes) total += s;
   if (o->pinned_cap_ < total) {
-    // the side stream holds the only readers and writers of the old buffer
+    // the side stream (or the SDMA queue) holds the only readers and writers of the old buffer
+    if (o->dma_) o->dma_->WaitAll();
     CheckHip(hipStreamSynchronize(o->side_), "checkpoint mirror drain");
     if (o->pinned_ != nullptr) (void)hipHostFree(o->pinned_);
     o->pinned_ = nullptr;
@@ -113,13 +142,25 @@ void DeviceCheckpoint::Half::StartMirror() const {
              "hipHostMalloc(mirror)");
     o->pinned_cap_ = std::max<size_t>(total, 1);
   }
+  if (o->dma_) {
+    // SDMA: jobs wait for the snapshot and run in order in the copier's thread
+    size_t at = 0;
+    ticket = 0;
+    for (size_t i = 0; i < sizes.size(); ++i) {
+      if (sizes[i] != 0) ticket = o->dma_->Submit(o->pinned_ + at, dev[i], sizes[i], snap_done);
+      at += sizes[i];
+    }
+    o->pinned_owner_ = this;
+    o->last_mirror_ = this;
+    return;
+  }
   // queued behind any earlier mirror on the same stream, so copies into the shared buffer
   // never overlap
   CheckHip(hipStreamWaitEvent(o->side_, snap_done, 0), "hipStreamWaitEvent(mirror)");
   size_t off = 0;
   for (size_t i = 0; i < sizes.size(); ++i) {
     if (sizes[i] != 0) {
-      CheckHip(o->mirror_ctas_ > 0
+      CheckHip(o->mirror_engine_ == kEngineKernel
                    ? LaunchCopyNarrow(o->pinned_ + off, dev[i], sizes[i], o->mirror_ctas_, o->side_)
                    : hipMemcpyAsync(o->pinned_ + off, dev[i], sizes[i], hipMemcpyDeviceToHost,
                                     o->side_),
@@ -134,7 +175,7 @@ void DeviceCheckpoint::Half::StartMirror() const {
 
 void DeviceCheckpoint::Half::Save(Stream *fo) const {
   if (!mirrored()) StartMirror();  // deferred mirror: a peer needs the bytes now
-  CheckHip(hipEventSynchronize(d2h_done), "checkpoint mirror wait");
+  owner->WaitMirror(*this);
   uint64_t ml = meta.size();
   fo->Write(&ml, sizeof(ml));
   if (ml != 0) fo->Write(meta.data(), ml);

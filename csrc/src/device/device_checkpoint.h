@@ -30,10 +30,12 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "device/device_plane.h"
+#include "device/dma_copier.h"
 #include "rabit/serializable.h"
 
 namespace rabit {
@@ -65,8 +67,13 @@ class DeviceCheckpoint {
   /*! \brief mirror policy */
   enum MirrorMode { kMirrorIdle = 0, kMirrorAlways = 1, kMirrorOff = 2 };
   void set_mirror_mode(int m) { mirror_mode_ = m; }
-  /*! \brief workgroups of the narrow D2H copy kernel of the host mirror; 0: hipMemcpyAsync */
-  void set_mirror_ctas(int c) { mirror_ctas_ = c; }
+  /*! \brief copy engine of the host mirror: hipMemcpyAsync, a narrow copy kernel, or an SDMA
+   *         engine driven through ROCr (dma_copier.h) */
+  enum MirrorEngine { kEngineHip = 0, kEngineKernel = 1, kEngineSdma = 2 };
+  /*! \brief choose the engine (before the first snapshot); ctas: the kernel's workgroups.
+   *         An SDMA copier that cannot start falls back to hipMemcpyAsync (logged). */
+  void set_mirror_engine(int engine, int ctas);
+  int mirror_engine() const { return dma_ ? kEngineSdma : mirror_engine_; }
   /*! \brief run the mirrors on a stream of the lowest priority (before the first snapshot) */
   void set_mirror_low_priority(bool low);
   /*! \brief snapshot slots: 2, 3, or 0 = by size (3 below three_slot_max bytes) */
@@ -101,6 +108,7 @@ class DeviceCheckpoint {
     std::vector<size_t> sizes;    // payload sizes of the current snapshot
     std::string meta;
     hipEvent_t d2h_done{nullptr};
+    mutable uint64_t ticket{0};     // SDMA engine: the mirror's last copy job (0: none)
     hipEvent_t snap_done{nullptr};  // the HBM snapshot of this slot is complete
     /*! \brief queue the D2H mirror of this slot into the shared pinned buffer (side stream) */
     void StartMirror() const;
@@ -125,7 +133,12 @@ class DeviceCheckpoint {
   size_t three_slot_max_{size_t(4) << 30};
   int cur_{-1};
   int mirror_mode_{kMirrorIdle};
-  int mirror_ctas_{0};
+  int mirror_engine_{kEngineHip};
+  int mirror_ctas_{16};
+  std::unique_ptr<DmaCopier> dma_;
+  /*! \brief the mirror of h has finished (non-blocking) / wait for it */
+  bool MirrorDone(const Half &h) const;
+  void WaitMirror(const Half &h) const;
   char *pinned_{nullptr};  // the host mirror, shared by the slots
   size_t pinned_cap_{0};
   const Half *pinned_owner_{nullptr};

@@ -323,14 +323,13 @@ __global__ __launch_bounds__(kBlock) void CopyTileKernel(uint4 *__restrict__ dst
 }
 
 /*!
- * Narrow copy for device -> pinned host memory (rabit_device_mirror_ctas > 0 for checkpoint
- * mirrors): `ctas` workgroups walk the buffer grid-stride, 4 x 16 B per lane in flight, with
- * nontemporal stores.  PCIe (~55 GB/s) bounds the copy, so a few workgroups reach it.  It is NOT
- * the default: hipMemcpyAsync D2H runs a blit kernel with one 512-lane workgroup on every CU,
- * and measured against 20 bf16 8192^3 GEMMs on the caller's stream (tools/mirror_probe.py,
- * profiles/r2_s15_mirror) the blit hides ~55 % of a 256 MiB mirror (16.6 -> 18.8 ms) while
- * this kernel at 4-1024 workgroups hides none (21.4-23.3 ms): a few CUs slowed for the whole
- * copy stretch the GEMM's last wave of tiles.
+ * Narrow copy for device -> pinned host memory (rabit_device_mirror_engine=kernel for
+ * checkpoint mirrors): `ctas` workgroups walk the buffer grid-stride, 4 x 16 B per lane in
+ * flight, with nontemporal stores.  PCIe (~55 GB/s) bounds the copy, so a few workgroups reach
+ * it.  It is NOT the default: measured against 20 bf16 8192^3 GEMMs on the caller's stream
+ * (tools/mirror_probe.py, profiles/r2_s15_mirror), a 256 MiB mirror by hipMemcpyAsync (a blit
+ * kernel in PyTorch processes) costs the step +0.4 %, by this kernel at 4-1024 workgroups
+ * 2.7-4 ms: a few CUs slowed for the whole copy stretch the GEMM's last wave of tiles.
  */
 __global__ __launch_bounds__(kBlock) void CopyNarrowKernel(uint4 *__restrict__ dst,
                                                           const uint4 *__restrict__ src,

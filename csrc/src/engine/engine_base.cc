@@ -150,6 +150,17 @@ void EngineBase::SetParam(const char *name, const char *val) {
                  "rabit_device_mirror_priority must be low or normal (got %s)", val);
     mirror_low_prio_ = !strcmp(val, "low");
   }
+  if (is("rabit_device_mirror_engine")) {
+    if (!strcmp(val, "hip")) {
+      mirror_engine_ = device::DeviceCheckpoint::kEngineHip;
+    } else if (!strcmp(val, "kernel")) {
+      mirror_engine_ = device::DeviceCheckpoint::kEngineKernel;
+    } else if (!strcmp(val, "sdma")) {
+      mirror_engine_ = device::DeviceCheckpoint::kEngineSdma;
+    } else {
+      utils::Error("rabit_device_mirror_engine must be hip, kernel or sdma (got %s)", val);
+    }
+  }
   if (is("rabit_device_mirror_ctas")) {
     mirror_ctas_ = atoi(val);
     utils::Check(mirror_ctas_ >= 0 && mirror_ctas_ <= 4096,
@@ -664,7 +675,7 @@ void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
-    dev_ckpt_->set_mirror_ctas(mirror_ctas_);
+    dev_ckpt_->set_mirror_engine(MirrorEngine(), mirror_ctas_);
     dev_ckpt_->set_mirror_low_priority(mirror_low_prio_);
     dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
@@ -686,7 +697,7 @@ int EngineBase::DevLoadCheckPoint(int n, void *const *ptrs, const size_t *nbytes
   if (!dev_ckpt_) {
     dev_ckpt_.reset(new device::DeviceCheckpoint(dev_.get()));
     dev_ckpt_->set_mirror_mode(ckpt_mirror_mode_);
-    dev_ckpt_->set_mirror_ctas(mirror_ctas_);
+    dev_ckpt_->set_mirror_engine(MirrorEngine(), mirror_ctas_);
     dev_ckpt_->set_mirror_low_priority(mirror_low_prio_);
     dev_ckpt_->set_slots(ckpt_slots_, ckpt_3slot_max_);
   }
@@ -768,6 +779,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"n_device_ops\":" << s.n_device_ops << ",\"n_shm_ops\":" << s.n_shm_ops
      << ",\"ckpt_mirrors\":" << (dev_ckpt_ ? dev_ckpt_->mirrors() : 0)
      << ",\"ckpt_mirrors_deferred\":" << (dev_ckpt_ ? dev_ckpt_->mirrors_deferred() : 0)
+     << ",\"ckpt_mirror_engine\":" << (dev_ckpt_ ? dev_ckpt_->mirror_engine() : MirrorEngine())
      << ",\"ckpt_slots\":" << (dev_ckpt_ ? dev_ckpt_->slots() : 0)
      << ",\"ckpt_hbm_bytes\":" << (dev_ckpt_ ? dev_ckpt_->reserved_bytes() : 0)
      << ",\"ckpt_pinned_bytes\":" << (dev_ckpt_ ? dev_ckpt_->pinned_bytes() : 0)

@@ -104,6 +104,13 @@ class EngineBase : public IEngine {
    */
   int DevGraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream,
                         std::string *why);
+  /*! \brief copy engine of the checkpoint host mirrors (rabit_device_mirror_engine; a
+   *         rabit_device_mirror_ctas > 0 alone selects the kernel engine) */
+  int MirrorEngine() const {
+    if (mirror_engine_ >= 0) return mirror_engine_;
+    return mirror_ctas_ > 0 ? device::DeviceCheckpoint::kEngineKernel
+                            : device::DeviceCheckpoint::kEngineHip;
+  }
   /*!
    * \brief checkpoint HBM buffers: HBM snapshot + async pinned mirror, registered as a lazy
    *        global checkpoint (see device/device_checkpoint.h).  nl > 0: lptrs are this rank's
@@ -242,7 +249,8 @@ class EngineBase : public IEngine {
   int ckpt_mirror_mode_{0};          // rabit_device_ckpt_mirror: 0 idle, 1 always, 2 off
   int ckpt_slots_{0};                // rabit_device_ckpt_slots: 2, 3, 0 = by size
   bool mirror_low_prio_{false};      // rabit_device_mirror_priority=low
-  int mirror_ctas_{0};               // rabit_device_mirror_ctas: D2H mirror kernel width (0: hipMemcpyAsync)
+  int mirror_ctas_{0};               // rabit_device_mirror_ctas: D2H mirror kernel width (> 0: kernel engine)
+  int mirror_engine_{-1};            // rabit_device_mirror_engine: hip / kernel / sdma (-1: by ctas)
   size_t ckpt_3slot_max_{size_t(4) << 30};  // by size: 3 slots below this many bytes
   size_t shm_min_{1u << 20};        // rabit_host_shm_min
   size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)

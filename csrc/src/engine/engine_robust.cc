@@ -517,7 +517,8 @@ void EngineRobust::LocalModelCheck(const Serializable *local_model) {
       // local tensors stay in HBM (replicated over xGMI); Serializable models in host memory
       const bool on_device = local_model == &dev_local_ && dev_ != nullptr;
       local_.Configure(num_local_replica_ + 1, on_device, on_device ? dev_->device() : -1);
-      local_.set_mirror_ctas(mirror_ctas_);
+      local_.set_mirror_ctas(MirrorEngine() == device::DeviceCheckpoint::kEngineKernel
+                                 ? std::max(mirror_ctas_, 1) : 0);
     } else {
       use_local_model_ = 0;
       num_local_replica_ = 0;

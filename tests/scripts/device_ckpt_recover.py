@@ -40,5 +40,6 @@ assert torch.all(w == wv), (float(w[0]), wv)
 assert torch.all(b == 4.5)
 st = rabit.stats()
 rabit.finalize()
-print("[%d] DEVCKPT OK slots=%d hbm=%d pinned=%d" % (rank, st["ckpt_slots"], st["ckpt_hbm_bytes"],
-                                                   st["ckpt_pinned_bytes"]), flush=True)
+print("[%d] DEVCKPT OK slots=%d hbm=%d pinned=%d engine=%d"
+      % (rank, st["ckpt_slots"], st["ckpt_hbm_bytes"], st["ckpt_pinned_bytes"],
+         st["ckpt_mirror_engine"]), flush=True)

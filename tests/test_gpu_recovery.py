@@ -58,20 +58,24 @@ def test_device_checkpoint_recovery_two_slots(replay):
     assert max(hbm) <= 2 * ((1 << 18) + 256), hbm
 
 
-@pytest.mark.parametrize("ctas", ["8", "0"])
-def test_device_checkpoint_mirror_copy_engines(ctas):
-    """the pinned host mirror written by the narrow copy kernel (rabit_device_mirror_ctas=8) or
-    by hipMemcpyAsync (0) is what a restarted rank gets over TCP (replay=0, every checkpoint
-    mirrored): its model must come back exactly"""
+@pytest.mark.parametrize("engine", ["kernel", "hip", "sdma"])
+def test_device_checkpoint_mirror_copy_engines(engine):
+    """the pinned host mirror written by each copy engine (a narrow copy kernel of 8
+    workgroups, hipMemcpyAsync, an SDMA engine driven through ROCr) is what a restarted rank
+    gets over TCP (replay=0, every checkpoint mirrored): its model must come back exactly"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import re
     script = os.path.join(ROOT, "tests", "scripts", "device_ckpt_recover.py")
     job = LocalJob([sys.executable, script, "mock=0,1,0,0", "mock=2,3,1,0",
-                    "rabit_device_ckpt_mirror=always", "rabit_device_mirror_ctas=" + ctas,
-                    "rabit_device_mirror_priority=low", "rabit_device_replay=0"], 3, 4,
-                   capture=True, timeout=240, print_fn=lambda m: None)
+                    "rabit_device_ckpt_mirror=always", "rabit_device_mirror_engine=" + engine,
+                    "rabit_device_mirror_ctas=8", "rabit_device_mirror_priority=low",
+                    "rabit_device_replay=0"], 3, 4, capture=True, timeout=240,
+                   print_fn=lambda m: None)
     rc = job.run()
     out = "".join("".join(o) for o in job.outputs)
     assert rc == 0, out[-4000:]
     assert out.count("DEVCKPT OK") == 3, out[-3000:]
     assert "reloaded version" in out
+    want = {"hip": "0", "kernel": "1", "sdma": "2"}[engine]
+    assert set(re.findall(r"engine=(\d)", out)) == {want}, out[-3000:]

@@ -19,7 +19,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def one(ctas, prio="normal", reps=5):
+def one(ctas, prio="normal", engine=None, mirror="always", reps=5):
     import numpy as np
     import torch
     sys.path.insert(0, ROOT)
@@ -29,8 +29,9 @@ def one(ctas, prio="normal", reps=5):
     tr = RabitTracker("127.0.0.1", 1, port=9391, port_end=9491, print_fn=lambda m: None).start(1)
     rabit.init(rabit_tracker_uri="127.0.0.1", rabit_tracker_port=tr.port, rabit_task_id=0,
                rabit_world_size=1, rabit_world1_fastpath=0, rabit_device=0,
-               rabit_device_ckpt_mirror="always", rabit_device_mirror_ctas=ctas,
-               rabit_device_mirror_priority=prio)
+               rabit_device_ckpt_mirror=mirror, rabit_device_mirror_ctas=ctas,
+               rabit_device_mirror_priority=prio,
+               **({"rabit_device_mirror_engine": engine} if engine else {}))
     model = torch.rand((256 << 20) // 4, device="cuda")
     a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
@@ -68,8 +69,11 @@ def one(ctas, prio="normal", reps=5):
     res = {k: round(float(np.median(v)) * 1e6, 1) for k, v in out.items()}
     res["mirror_ctas"] = ctas
     res["priority"] = prio
+    res["engine"] = engine or ("kernel" if ctas > 0 else "hip")
+    res["mirror"] = mirror
     res["hsa_enable_sdma"] = os.environ.get("HSA_ENABLE_SDMA")
     res["stats_mirrors"] = rabit.stats().get("ckpt_mirrors")
+    res["stats_engine"] = rabit.stats().get("ckpt_mirror_engine")
     print("MIRROR " + json.dumps(res), flush=True)
     rabit.finalize()
     tr.join(10)
@@ -77,10 +81,13 @@ def one(ctas, prio="normal", reps=5):
 
 def main():
     if len(sys.argv) > 1:
-        one(int(sys.argv[1]), sys.argv[2] if len(sys.argv) > 2 else "normal")
+        one(int(sys.argv[1]), sys.argv[2] if len(sys.argv) > 2 else "normal",
+            sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] != "-" else None,
+            sys.argv[4] if len(sys.argv) > 4 else "always")
         return
     # "N", "N:sdma" (HSA_ENABLE_SDMA=1 for that run: the runtime may move the D2H copy to a
-    # DMA engine instead of a blit kernel) or "N:low" (mirror stream of the lowest priority)
+    # DMA engine instead of a blit kernel), "N:low" (mirror stream of the lowest priority) or
+    # "0:engine=sdma" (rabit_device_mirror_engine); ":off" takes no mirror at all (baseline)
     settings = os.environ.get("MIRROR_SETTINGS", "0,4,8,16,32,64").split(",")
     for setting in settings:
         ctas = int(setting.split(":")[0])
@@ -88,8 +95,10 @@ def main():
         if setting.endswith(":sdma"):
             env["HSA_ENABLE_SDMA"] = "1"
         prio = "low" if setting.endswith(":low") else "normal"
-        r = subprocess.run([sys.executable, __file__, str(ctas), prio], capture_output=True,
-                           text=True, timeout=300, env=env)
+        engine = setting.split("engine=")[1].split(":")[0] if "engine=" in setting else "-"
+        mirror = "off" if setting.endswith(":off") else "always"
+        r = subprocess.run([sys.executable, __file__, str(ctas), prio, engine, mirror],
+                           capture_output=True, text=True, timeout=300, env=env)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("MIRROR ")]
         if r.returncode != 0 or not lines:
             print("ctas=%d failed rc=%d\n%s" % (ctas, r.returncode, r.stderr[-2000:]), flush=True)
