@@ -107,6 +107,15 @@ void DmaCopier::Wait(uint64_t ticket) {
   utils::Check(!failed_, "SDMA mirror copy failed");
 }
 
+void DmaCopier::WaitAll() {
+  uint64_t last;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    last = submitted_;
+  }
+  Wait(last);
+}
+
 void DmaCopier::Run() {
   hsa_signal_t sig;
   const bool have_sig = hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS;

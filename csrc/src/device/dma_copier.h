@@ -46,7 +46,7 @@ class DmaCopier {
   /*! \brief block until the job with this ticket has finished; fails loudly if a copy failed */
   void Wait(uint64_t ticket);
   /*! \brief block until every queued job has finished */
-  void WaitAll() { Wait(submitted_); }
+  void WaitAll();
 
  private:
   struct Job {
