@@ -1,6 +1,7 @@
 """allreduce_graphable inside a captured hipGraph (base engine, one GPU): the world-1 transport
-hook gives the rank a one-rank RCCL communicator, so the captured step holds a real
-ncclAllReduce node between the step's kernels.  Replays must give the eager result every time;
+hook gives the rank a one-rank RCCL communicator, so ncclAllReduce is called on the capturing
+stream between the step's kernels (for one rank RCCL records it as a copy, not a reduction
+kernel: this checks the API's capture and replay path).  Replays must give the eager result every time;
 the fault-tolerant engines and BitOR must be refused.  argv[1]: base | standard."""
 import sys
 
