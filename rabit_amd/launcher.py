@@ -1,5 +1,5 @@
-"""Job launcher with restart-on-failure (the role of `dmlc-submit --cluster local|ssh`, which
-the reference's test/test.mk and guide use).
+"""Job launcher with restart-on-failure (the role of `dmlc-submit --cluster local|ssh|mpi`,
+which the reference's test/test.mk and guide use; plus Slurm).
 
 Starts a tracker, spawns `num_workers` copies of a command with the DMLC_* environment and
 restarts any worker that exits with a non-zero status, up to `num_attempt` times, passing the
@@ -13,7 +13,8 @@ of the file, `host[:slots]` or `host slots=N` per line.  Ranks fill each host's 
 next host, so ranks that share a node are consecutive (their ring links and the direct device
 transport stay on xGMI); every worker gets LOCAL_RANK / LOCAL_WORLD_SIZE for its node, from
 which the device plane picks its GPU (one process per GPU).  The tracker listens on --host-ip,
-by default this host's address.
+by default this host's address.  A remote worker ends with its ssh session, so a killed
+launcher leaves nothing running on the hosts.
 
     python -m rabit_amd.launcher --cluster ssh --host-file hosts -n 16 -- python train.py
 
