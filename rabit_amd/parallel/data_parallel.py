@@ -91,9 +91,22 @@ class GradientBuckets:
         if dst:
             torch._foreach_copy_(dst, src)
 
-    def reduce(self, op: int = rabit.SUM):
-        """Allreduce every bucket (in place); returns the buckets."""
+    def reduce(self, op: int = rabit.SUM, graphable: bool = False):
+        """Allreduce every bucket (in place); returns the buckets.
+
+        graphable=True: HBM buckets go through `rabit.allreduce_graphable` (a bare in-place
+        ncclAllReduce on the current stream, no host synchronisation), so the call can sit
+        inside a captured hipGraph with the rest of the step.  Non-fault-tolerant engines only
+        (init(lib="base")); averaging is one `mul_` on the same stream, captured as well."""
         world = rabit.get_world_size()
+        if graphable:
+            for b in self.buckets:
+                if not b.is_cuda:
+                    raise TypeError("graphable reduce needs HBM buckets")
+                rabit.allreduce_graphable(b, op)
+                if self.average and op == rabit.SUM and world > 1:
+                    b.mul_(1.0 / world)
+            return self.buckets
         for b in self.buckets:
             if b.is_cuda and self.average and op == rabit.SUM and world > 1:
                 rabit.allreduce_prepared(b, b, op, rabit.PREP_SCALE, 1.0 / world)

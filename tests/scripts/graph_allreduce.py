@@ -59,6 +59,36 @@ for i in range(4):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(z, x * 2.0 + 1.0), ("replay", i)
+# the whole data-parallel step in one graph: forward, backward into the buckets, bucket allreduce
+from rabit_amd.parallel import GradientBuckets  # noqa: E402
+
+torch.manual_seed(0)
+model = torch.nn.Sequential(torch.nn.Linear(64, 64, bias=False), torch.nn.Tanh(),
+                            torch.nn.Linear(64, 8, bias=False)).to(dev)
+buckets = GradientBuckets(model.parameters(), bucket_mb=1.0)
+xs = torch.randn(32, 64, device=dev)
+
+
+def dp_step():
+    loss = model(xs).square().mean()
+    buckets.backward(loss)
+    buckets.reduce(graphable=True)
+    return loss
+
+
+with torch.cuda.stream(side):
+    for _ in range(2):
+        dp_step()
+torch.cuda.current_stream().wait_stream(side)
+eager = [b.clone() for b in buckets.buckets]
+g2 = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g2):
+    dp_step()
+for b in buckets.buckets:
+    b.zero_()
+g2.replay()
+torch.cuda.synchronize()
+assert all(torch.equal(a, b) for a, b in zip(eager, buckets.buckets)), "graphed DP step"
 assert rabit.stats()["device_rccl"] == 1, "no RCCL communicator: nothing was captured"
 print("GRAPHAR OK", flush=True)
 rabit.finalize()
