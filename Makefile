@@ -70,13 +70,18 @@ $(LIBDIR)/librabit_mock.a: $(CORE_OBJS) $(KERN_OBJ) $(OBJ)/registry_mock.o
 	rm -f $@ && ar rcs $@ $^
 
 # ---------------------------------------------------------------- test / example programs
-TEST_PROGS := unit_tests recover_test speed_test basic broadcast lazy_allreduce device_reducer_test
+TEST_PROGS := unit_tests recover_test speed_test basic broadcast lazy_allreduce device_reducer_test \
+              rccl_lifecycle_test
 tests: $(foreach p,$(TEST_PROGS),$(BIN)/$(p))
 
 # -Wno-array-bounds -Wno-stringop-overflow: a test writes past a fixed buffer on purpose (the write throws first)
 $(BIN)/unit_tests: tests/cpp/unit_tests.cc $(LIBDIR)/librabit_mock.a $(HEADERS)
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) -Wno-array-bounds -Wno-stringop-overflow $< $(LIBDIR)/librabit_mock.a -o $@ $(LDLIBS)
+# GPU test of the RCCL communicator lifecycle: drives DevicePlane directly (internal API)
+$(BIN)/rccl_lifecycle_test: tests/cpp/rccl_lifecycle_test.cc $(LIBDIR)/librabit_mock.a $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) $(CXXFLAGS) $< $(LIBDIR)/librabit_mock.a -o $@ $(LDLIBS)
 # a HIP program: the user's reduction is instantiated as a gfx950 kernel in its own TU
 $(BIN)/device_reducer_test: tests/cpp/device_reducer_test.hip $(LIBDIR)/librabit_mock.so $(HEADERS)
 	@mkdir -p $(BIN)

@@ -18,9 +18,12 @@ engine's bookkeeping plus its HBM result-log copy (rabit_world1_fastpath=0), rep
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8
 
-Rank 0 prints one JSON line.  `value` is the whole-job aggregate throughput N * S / t
-(GB/s, S = 128 MiB per rank, weak scaling); nccl-tests style `busbw_GBps` / `algbw_GBps` and
-the per-step wall clock are reported alongside.  The whole run is under a wall-clock deadline
+Rank 0 prints one JSON line.  `value` is BASELINE.json's metric, the allreduce BUS bandwidth
+(nccl-tests: busbw = algbw * 2(N-1)/N, algbw = S / t, S = 128 MiB per rank, weak scaling) at
+N > 1.  At N = 1 busbw is 0 by definition (no byte crosses a link), so `value` is the algbw of
+the robust engine's local op and `collective` is false; `value_is` names which one it is.  The
+per-step wall clock, algbw, the whole-job aggregate N * S / t and the reference's own
+`sum_tdiff-speed` (per-rank MiB/s, test/speed_test.cc:52-69) are reported alongside.  The whole run is under a wall-clock deadline
 (--deadline): a rank that exceeds it names the phase it was in and exits non-zero.  The side
 measurements after the headline (variants, extras) have a budget of their own (--post-deadline)
 and cannot take the measured headline with them: an exception in one is recorded in
@@ -240,7 +243,10 @@ def run_extras(rabit, torch, dev, world):
                                                if world > 1 else None)
     rabit.checkpoint(None)
     del hb
-    # config 5 (checkpoint part): HBM snapshot of a 256 MiB model every iteration
+    # config 5: 256 MiB sum + checkpoint every iteration, against the sum alone
+    out.update(run_config5(rabit, torch, dev))
+    rabit.checkpoint(None)
+    # config 5 (checkpoint part alone): HBM snapshot of a 256 MiB model
     model = torch.rand((256 << 20) // 4, dtype=torch.float32, device=dev)
     rabit.checkpoint_tensors({"w": model}, meta={"it": 0})
     # iterations longer than the async D2H mirror (~5 ms for 256 MiB) see only the snapshot
@@ -251,8 +257,23 @@ def run_extras(rabit, torch, dev, world):
     return out
 
 
-def time_steps(rabit, torch, x, steps):
-    """wall time of `steps` back-to-back allreduces, ranks in lock step, max over ranks"""
+def bandwidths(world, size_bytes, t_step):
+    """the headline numbers of one timed step of t_step seconds: nccl-tests algbw / busbw, the
+    whole-job aggregate, and `value` (busbw at N > 1; algbw at N = 1, where busbw is 0)"""
+    algbw = size_bytes / t_step / 1e9
+    busbw = algbw * (2.0 * (world - 1) / world) if world > 1 else 0.0
+    out = {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
+           "aggregate_GBps": round(world * size_bytes / t_step / 1e9, 2)}
+    if world > 1:
+        out["value"], out["value_is"] = out["busbw_GBps"], "busbw_GBps"
+    else:
+        out["value"], out["value_is"] = out["algbw_GBps"], "algbw_GBps (N=1: busbw is 0 by definition)"
+    return out
+
+
+def time_steps(rabit, torch, x, steps, with_mean=False):
+    """wall time of `steps` back-to-back allreduces, ranks in lock step, max over ranks
+    (with_mean: also the mean over ranks, as the reference's speed_test averages)"""
     torch.cuda.synchronize()
     rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
     torch.cuda.synchronize()
@@ -263,7 +284,41 @@ def time_steps(rabit, torch, x, steps):
     rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    return float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
+    worst = float(rabit.allreduce(np.array([elapsed]), rabit.MAX)[0])
+    if not with_mean:
+        return worst
+    mean = float(rabit.allreduce(np.array([elapsed]), rabit.SUM)[0]) / rabit.get_world_size()
+    return worst, mean
+
+
+def run_config5(rabit, torch, dev, iters=5):
+    """BASELINE.json config 5 without the kill: every iteration allreduces a 256 MiB float32
+    gradient through the robust engine, applies it to a 256 MiB model and checkpoints the model
+    (HBM snapshot + async host mirror, reference flow src/allreduce_robust.cc:484-557).  The
+    same loop without the checkpoint gives the checkpoint's overhead.  Ranks in lock step, median
+    iteration, max over ranks.  The kill/recover timing is tools/robust_bench.py's job."""
+    n = (256 << 20) // 4
+    grad = torch.rand(n, dtype=torch.float32, device=dev).mul_(1e-3)
+    model = torch.zeros(n, dtype=torch.float32, device=dev)
+    it = [0]
+
+    def step(ckpt):
+        rabit.allreduce(grad, rabit.SUM)
+        model.add_(grad, alpha=-1e-3)
+        if ckpt:
+            it[0] += 1
+            rabit.checkpoint_tensors({"w": model}, meta={"it": it[0]})
+
+    step(True)
+    t_ckpt = _timed(rabit, torch, lambda: step(True), iters)
+    # the same iterations without the checkpoint (their results stay in the HBM log until the
+    # checkpoint after the loop: iters x 256 MiB)
+    step(False)
+    t_sum = _timed(rabit, torch, lambda: step(False), iters)
+    rabit.checkpoint(None)
+    del grad, model
+    return {"config5_iter_us": round(t_ckpt * 1e6, 1), "config5_sum_only_iter_us": round(t_sum * 1e6, 1),
+            "config5_ckpt_overhead_us": round((t_ckpt - t_sum) * 1e6, 1), "config5_iters": iters}
 
 
 def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=False):
@@ -438,18 +493,16 @@ def main():
     for _ in range(args.warmup):
         rabit.allreduce(x, rabit.SUM)
     phase("timed")
-    elapsed = time_steps(rabit, torch, x, args.steps)
+    elapsed, elapsed_mean = time_steps(rabit, torch, x, args.steps, with_mean=True)
     st_head = rabit.stats()
 
     t_step = elapsed / args.steps
     size_bytes = n * 4
-    algbw = size_bytes / t_step / 1e9
-    busbw = algbw * (2.0 * (world - 1) / world) if world > 1 else 0.0
-    aggregate = world * size_bytes / t_step / 1e9
+    bw = bandwidths(world, size_bytes, t_step)
     st = st_head
     rec = {
-        "metric": "allreduce_128MB_fp32_sum_throughput",
-        "value": round(aggregate, 2),
+        "metric": "allreduce_128MB_fp32_sum_busbw",
+        "value": bw["value"],
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -464,12 +517,16 @@ def main():
                    "global_batch": world, "seq_len": n, "parallelism": "dp%d" % world,
                    "engine": args.engine, "size_bytes_per_rank": size_bytes,
                    "input_buffer": "symmetric heap" if args.symmetric else "torch allocation"},
-        "busbw_GBps": round(busbw, 2),
-        "algbw_GBps": round(algbw, 2),
+        "value_is": bw["value_is"],
+        "busbw_GBps": bw["busbw_GBps"],
+        "algbw_GBps": bw["algbw_GBps"],
         "t_us": round(t_step * 1e6, 1),
+        "aggregate_GBps": bw["aggregate_GBps"],
+        # the reference's own number (test/speed_test.cc:52-69): S / mean-over-ranks time, MiB/s
+        "sum_tdiff_speed_MiBps": round(size_bytes * args.steps / elapsed_mean / 2 ** 20, 1),
         "collective": world > 1,
-        "value_definition": "N * bytes_per_rank / t_step (whole-job reduced bytes per second); "
-                            "busbw = algbw * 2(N-1)/N as nccl-tests",
+        "value_definition": "busbw = algbw * 2(N-1)/N as nccl-tests, algbw = bytes_per_rank / "
+                            "t_step (N=1: algbw); aggregate_GBps = N * bytes_per_rank / t_step",
         "baseline_note": "reference publishes no numbers (BASELINE.md)",
         "result_check": "bit-exact vs host fp64 reference" if checked else None,
         "check_fallback": check_fallback,
@@ -493,7 +550,7 @@ def main():
         "variants": None,
         "direct_phase_breakdown": None,
         "extras": None,
-        "reference_measured": reference_measured(world, aggregate),
+        "reference_measured": reference_measured(world, bw["aggregate_GBps"]),
     }
     if world == 1:
         rec["n1_note"] = ("N=1: no data moves between ranks; the step is the robust engine's "

@@ -29,6 +29,8 @@ struct WaitState {
   std::atomic<int> wait_depth{0};      // > 0: blocked on peers, the device or the tracker
   std::atomic<double> working_since{0};  // start of the current working stretch (0: none)
   std::atomic<double> device_wait_since{0};  // start of the current wait on the GPU (0: none)
+  std::atomic<double> device_op_deadline{0};  // deadline (s) of the device op being waited
+                                              // for, which aborts it on its own (0: none)
 };
 
 inline WaitState &GlobalWaitState() {
@@ -97,6 +99,28 @@ inline double DeviceWaitingFor() {
   const double since = GlobalWaitState().device_wait_since.load();
   return since > 0 ? MonotonicSec() - since : 0.0;
 }
+
+/*!
+ * \brief the limit the watchdog applies to a wait on this rank's GPU: the configured device
+ *        wait limit, but never below the deadline of the device op being waited for plus the
+ *        drain time its abort may take (that wait includes peers' barriers and RCCL, so a healthy
+ *        rank waiting on a slow peer must reach its own op deadline first).  0: no limit.
+ */
+inline double EffectiveDeviceWaitLimit(double wait_limit, double op_deadline, double drain_sec) {
+  if (wait_limit <= 0) return 0.0;
+  if (op_deadline <= 0) return wait_limit;
+  const double own = op_deadline + drain_sec + 5.0;
+  return own > wait_limit ? own : wait_limit;
+}
+
+/*! \brief marks the deadline of the device op a wait is for (see EffectiveDeviceWaitLimit) */
+class DeviceDeadlineScope {
+ public:
+  explicit DeviceDeadlineScope(double sec) { GlobalWaitState().device_op_deadline.store(sec); }
+  ~DeviceDeadlineScope() { GlobalWaitState().device_op_deadline.store(0.0); }
+  DeviceDeadlineScope(const DeviceDeadlineScope &) = delete;
+  DeviceDeadlineScope &operator=(const DeviceDeadlineScope &) = delete;
+};
 
 /*! \brief seconds this rank has been working inside an op without waiting (0: not) */
 inline double WorkingFor() {

@@ -58,14 +58,29 @@ bool DeviceCheckpoint::MirrorDone(const Half &h) const {
 
 void DeviceCheckpoint::WaitMirror(const Half &h) const {
   if (dma_) {
-    dma_->Wait(h.ticket);
+    if (!dma_->Wait(h.ticket) && pinned_owner_ == &h) {
+      // the copier could not deliver this mirror: redo it synchronously on the side stream so
+      // a Save of these bytes reads a complete host copy
+      utils::HandleLogInfo("[xrabit] checkpoint mirror failed on the SDMA path: redone with "
+                           "hipMemcpyAsync\n");
+      size_t off = 0;
+      for (size_t i = 0; i < h.sizes.size(); ++i) {
+        if (h.sizes[i] != 0) {
+          CheckHip(hipMemcpyAsync(pinned_ + off, h.dev[i], h.sizes[i], hipMemcpyDeviceToHost,
+                                  side_),
+                   "D2H mirror (redo)");
+        }
+        off += h.sizes[i];
+      }
+      CheckHip(hipStreamSynchronize(side_), "checkpoint mirror redo");
+    }
     return;
   }
   CheckHip(hipEventSynchronize(h.d2h_done), "checkpoint mirror wait");
 }
 
 DeviceCheckpoint::~DeviceCheckpoint() {
-  if (dma_) dma_->WaitAll();
+  if (dma_) (void)dma_->WaitAll();
   dma_.reset();
   (void)hipStreamSynchronize(side_);
   for (auto &h : half_) {
@@ -133,7 +148,7 @@ void DeviceCheckpoint::Half::StartMirror() const {
   for (size_t s : sizes) total += s;
   if (o->pinned_cap_ < total) {
     // the side stream (or the SDMA queue) holds the only readers and writers of the old buffer
-    if (o->dma_) o->dma_->WaitAll();
+    if (o->dma_) (void)o->dma_->WaitAll();  // the old buffer is dropped: failures do not matter
     CheckHip(hipStreamSynchronize(o->side_), "checkpoint mirror drain");
     if (o->pinned_ != nullptr) (void)hipHostFree(o->pinned_);
     o->pinned_ = nullptr;

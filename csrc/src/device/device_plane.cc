@@ -12,8 +12,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <thread>
 
+#include "core/trace.h"
 #include "core/wait_state.h"
 #include "device/kernels.h"
 #include "rabit/internal/half.h"
@@ -181,6 +185,10 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   }
   device_ = dev % ndev;
   CheckHip(hipSetDevice(device_), "hipSetDevice");
+  // connect RCCL's collective channels at communicator init (InitComm's helper thread, watched
+  // by the failure probe) instead of lazily inside the first collective that needs them, where
+  // a dead peer would block the enqueueing thread with no deadline.  A user setting wins.
+  setenv("NCCL_RUNTIME_CONNECT", "0", 0);
   CheckHip(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   CheckHip(hipEventCreateWithFlags(&ev_switch_, hipEventDisableTiming), "hipEventCreate");
   stream_ = cfg_.ops_on_user_stream ? user_stream_ : own_stream_;
@@ -215,13 +223,28 @@ DevicePlane::~DevicePlane() {
   (void)hipDeviceSynchronize();
   peers_.reset();
   if (comm_ != nullptr) {
-    ncclCommDestroy(comm_);
+    // flush and release it; a non-blocking communicator finalizes asynchronously (bounded
+    // wait: a peer that is gone must not hold this process at exit)
+    ncclResult_t r = ncclCommFinalize(comm_);
+    ncclResult_t st = r;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress && ncclCommGetAsyncError(comm_, &st) == ncclSuccess &&
+           st == ncclInProgress &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10)) {
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if ((r == ncclSuccess || r == ncclInProgress) && st == ncclSuccess) {
+      ncclCommDestroy(comm_);
+    } else {
+      ncclCommAbort(comm_);
+    }
     comm_ = nullptr;
   }
   for (int i = 0; i < kScratchSlots; ++i) {
     if (scratch_[i] != nullptr) (void)hipFree(scratch_[i]);
   }
   if (pinned_ != nullptr) (void)hipHostFree(pinned_);
+  if (warm_ != nullptr) (void)hipFree(warm_);
   if (ev_in_ != nullptr) (void)hipEventDestroy(ev_in_);
   if (ev_done_ != nullptr) (void)hipEventDestroy(ev_done_);
   peers_.reset();
@@ -247,9 +270,24 @@ std::string DevicePlane::NewUniqueId() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+namespace {
+/*!
+ * \brief state shared by the thread that waits for a communicator's bring-up and the helper
+ *        thread that runs it.  The helper may outlive the waiter's interest (a peer died inside
+ *        RCCL's bootstrap, which waits on sockets without any deadline): the waiter then
+ *        abandons it, and a helper that ever returns aborts the communicator it built itself.
+ */
+struct CommBringUp {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done{false}, abandoned{false};
+  ncclResult_t result{ncclSuccess};
+  ncclComm_t comm{nullptr};
+};
+}  // namespace
+
 Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
                              const FailureProbe &probe) {
-  (void)probe;
   if (comm_ != nullptr) AbortComm();
   utils::Check(id_bytes.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
   ncclUniqueId id;
@@ -261,15 +299,205 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
   if (cfg_.rccl_min_ctas > 0) config.minCTAs = cfg_.rccl_min_ctas;
   if (cfg_.rccl_max_ctas > 0) config.maxCTAs = cfg_.rccl_max_ctas;
   config.commName = "xrabit";
-  ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &config);
-  if (r != ncclSuccess) {
+  // Blocking communicator, brought up on a helper thread.  RCCL 2.27's non-blocking mode does
+  // not help here: ncclCommInitRankConfig with blocking = 0 still blocks the caller inside the
+  // bootstrap while a rank is missing (measured: profiles/r3_rccl_lifecycle/).  The helper runs
+  // the init and then connects every channel this job will use (eager collective connections,
+  // NCCL_RUNTIME_CONNECT=0, set by the constructor; plus one grouped send/recv with every peer
+  // and a one-element allreduce), all while the ranks are known to be alive.  Afterwards no
+  // RCCL call of this epoch waits on a peer on the host: only kernels do, and WaitEvent aborts
+  // those.  This thread meanwhile watches the failure probe and the deadline.
+  config.blocking = 1;
+  if (warm_ == nullptr) CheckHip(hipMalloc(&warm_, 4096), "hipMalloc(rccl warm-up)");
+  auto g = std::make_shared<CommBringUp>();
+  const int dev = device_;
+  hipStream_t ws = own_stream_;
+  char *wbuf = static_cast<char *>(warm_);
+  std::thread([g, id, nranks, rank, config, dev, ws, wbuf]() mutable {
+    (void)hipSetDevice(dev);
+    ncclComm_t c = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &config);
+    if (r == ncclSuccess && nranks > 1) {
+      // every p2p pair (RCCL connects send/recv channels lazily inside ncclGroupEnd) and the
+      // allreduce path, with 1-byte / 1-element payloads
+      r = ncclGroupStart();
+      for (int p = 0; p < nranks && r == ncclSuccess; ++p) {
+        if (p == rank) continue;
+        r = ncclSend(wbuf + 64 * (p % 32), 1, ncclUint8, p, c, ws);
+        if (r == ncclSuccess) r = ncclRecv(wbuf + 2048 + 64 * (p % 32), 1, ncclUint8, p, c, ws);
+      }
+      const ncclResult_t e = ncclGroupEnd();
+      if (r == ncclSuccess) r = e;
+      if (r == ncclSuccess) {
+        r = ncclAllReduce(wbuf + 4088, wbuf + 4088, 1, ncclFloat32, ncclSum, c, ws);
+      }
+    }
+    bool abandoned;
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->comm = c;
+      g->result = r;
+      g->done = true;
+      abandoned = g->abandoned;
+    }
+    g->cv.notify_all();
+    if (abandoned && c != nullptr) ncclCommAbort(c);  // nobody else will ever use it
+  }).detach();
+  core::WaitScope waiting;  // the bootstrap waits on every peer
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  const double limit = cfg_.comm_init_timeout_sec;
+  bool done = false;
+  Status fail = Status::kSuccess;
+  {
+    std::unique_lock<std::mutex> lk(g->mu);
+    for (;;) {
+      g->cv.wait_for(lk, std::chrono::milliseconds(2), [&]() { return g->done; });
+      if (g->done) {
+        done = true;
+        break;
+      }
+      const double waited = std::chrono::duration<double>(clock::now() - t0).count();
+      if (probe && waited > 1e-3) {
+        lk.unlock();
+        const bool dead = probe();
+        lk.lock();
+        if (g->done) {
+          done = true;
+          break;
+        }
+        if (dead) {
+          fail = Status::kAborted;
+          break;
+        }
+      }
+      if (limit > 0 && waited > limit) {
+        fail = Status::kTimeout;
+        break;
+      }
+    }
+    if (!done) g->abandoned = true;  // the helper aborts what it built, if it ever returns
+  }
+  if (!done) {
+    rccl_aborts_ += 1;
+    init_abandoned_ += 1;
+    utils::HandleLogInfo("[xrabit] RCCL communicator bring-up %s after %.1f s: abandoned (the "
+                         "helper thread stays blocked in RCCL's bootstrap)\n",
+                         fail == Status::kTimeout ? "timed out" : "lost a peer",
+                         std::chrono::duration<double>(clock::now() - t0).count());
+    return fail;
+  }
+  comm_ = g->comm;
+  if (g->result != ncclSuccess) {
+    utils::HandleLogInfo("[xrabit] RCCL communicator bring-up failed: %s\n",
+                         ncclGetErrorString(g->result));
+    if (comm_ != nullptr) {
+      rccl_aborts_ += 1;
+      AbortComm();  // drains the warm-up kernels the helper may have enqueued
+    }
     comm_ = nullptr;
-    utils::HandleLogInfo("[xrabit] ncclCommInitRankConfig failed: %s\n", ncclGetErrorString(r));
     return Status::kAborted;
   }
   nranks_ = nranks;
   rank_ = rank;
+  if (nranks > 1) {
+    // the warm-up kernels need every peer as well: wait like for any collective (probe,
+    // deadline, abort on failure)
+    hipEvent_t ev = nullptr;
+    CheckHip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(warm-up)");
+    CheckHip(hipEventRecord(ev, own_stream_), "hipEventRecord(warm-up)");
+    op_bytes_ = 0;
+    const Status s = WaitEvent(ev, probe);
+    (void)hipEventDestroy(ev);
+    if (s != Status::kSuccess) return s;  // WaitEvent aborted the communicator
+  }
   return Status::kSuccess;
+}
+
+bool DevicePlane::MockRcclFault() {
+  rccl_calls_ += 1;
+  if (cfg_.mock_rccl_error > 0 && rccl_calls_ == static_cast<uint64_t>(cfg_.mock_rccl_error)) {
+    utils::HandleLogInfo("[xrabit] mock: RCCL call %llu fails with ncclRemoteError\n",
+                         static_cast<unsigned long long>(rccl_calls_));
+    return true;
+  }
+  return false;
+}
+
+Status DevicePlane::FailRccl(const char *what, int result) {
+  const ncclResult_t r = static_cast<ncclResult_t>(result);
+  if (ClassifyRccl(result) == RcclOutcome::kFatal) {
+    utils::Error("RCCL error in %s: %s", what, ncclGetErrorString(r));
+  }
+  rccl_aborts_ += 1;
+  rccl_fail_streak_ += 1;
+  utils::Check(cfg_.rccl_max_failures <= 0 || rccl_fail_streak_ <= cfg_.rccl_max_failures,
+               "RCCL failed %d times in a row (last: %s in %s); giving up", rccl_fail_streak_,
+               ncclGetErrorString(r), what);
+  utils::HandleLogInfo("[xrabit] RCCL %s in %s: aborting the communicator, recovering\n",
+                       ncclGetErrorString(r), what);
+  AbortComm();
+  return Status::kAborted;
+}
+
+Status DevicePlane::Settle(const char *what, const FailureProbe &probe, double limit_sec) {
+  core::WaitScope waiting;  // RCCL init / lazy connection setup waits on the peers
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  rccl_settled_ += 1;
+  for (uint64_t iter = 0;; ++iter) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclSuccess) return Status::kSuccess;
+    if (st != ncclInProgress) return FailRccl(what, st);
+    const double waited = std::chrono::duration<double>(clock::now() - t0).count();
+    if (probe && (iter & 7) == 0 && waited > 1e-3 && probe()) {
+      utils::HandleLogInfo("[xrabit] a peer failed during %s: aborting the communicator\n", what);
+      rccl_aborts_ += 1;
+      AbortComm();
+      return Status::kAborted;
+    }
+    if (limit_sec > 0 && waited > limit_sec) {
+      utils::HandleLogInfo("[xrabit] %s did not complete within %.1f s: aborting the "
+                           "communicator\n", what, limit_sec);
+      rccl_aborts_ += 1;
+      AbortComm();
+      return Status::kTimeout;
+    }
+    // lazy connection setup takes milliseconds: spin briefly, then poll every 100 us
+    if (waited > 2e-4) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+
+Status DevicePlane::Rccl(int result, const char *what, const FailureProbe &probe) {
+  switch (ClassifyRccl(result)) {
+    case RcclOutcome::kOk: return Status::kSuccess;
+    case RcclOutcome::kPending: {
+      const double limit =
+          cfg_.op_timeout_sec < 0 ? AutoOpDeadline(op_bytes_) : cfg_.op_timeout_sec;
+      return Settle(what, probe, limit);
+    }
+    default: return FailRccl(what, result);
+  }
+}
+
+Status DevicePlane::RunP2P(const std::vector<P2POp> &ops,
+                           const std::function<char *(size_t, const P2POp &)> &at,
+                           const char *what, const FailureProbe &probe) {
+  if (ops.empty()) return Status::kSuccess;
+  if (MockRcclFault()) return FailRccl(what, ncclRemoteError);
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return Rccl(r, what, probe);
+  for (size_t i = 0; i < ops.size() && r == ncclSuccess; ++i) {
+    const P2POp &o = ops[i];
+    char *p = at(i, o);
+    r = o.send ? ncclSend(p, o.bytes, ncclUint8, o.peer, comm_, stream_)
+               : ncclRecv(p, o.bytes, ncclUint8, o.peer, comm_, stream_);
+  }
+  // the group is always closed (a failed call inside it is reported by ncclGroupEnd too)
+  const ncclResult_t e = ncclGroupEnd();
+  return Rccl(r != ncclSuccess ? r : e, what, probe);
 }
 
 void DevicePlane::AbortComm() {
@@ -486,11 +714,13 @@ void DevicePlane::EnterFromUser() {
 }
 
 Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
+  trace::Scope ts("device_wait", rank_, -1, -1, op_bytes_, 1);
   core::WaitScope waiting;  // peers' barriers and RCCL: waiting on other ranks
   core::DeviceWaitScope on_gpu;
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   const double limit = cfg_.op_timeout_sec < 0 ? AutoOpDeadline(op_bytes_) : cfg_.op_timeout_sec;
+  core::DeviceDeadlineScope deadline(limit);  // the watchdog leaves this wait to the deadline
   for (uint64_t iter = 0;; ++iter) {
     hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) {
@@ -542,6 +772,7 @@ Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
     s = WaitEvent(ev_done_, probe);
   }
   op_bytes_ = 0;
+  if (s == Status::kSuccess) rccl_fail_streak_ = 0;
   if (pending_dst_ != nullptr) {
     if (s == Status::kSuccess) CopyDeviceAsync(pending_dst_, pending_src_, pending_bytes_);
     pending_dst_ = nullptr;
@@ -609,12 +840,19 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   // a scaling prepare of a floating sum rides on RCCL's pre-multiplied sum (no extra pass)
   const bool premul = prep == kPrepScale && op == 2 &&
                       (dtype == 6 || dtype == 7 || dtype == 10 || dtype == 11);
-  if (prep != kPrepCopy && !premul) {
-    CheckHip(LaunchPrepare(recv, nullptr, send, count, dtype, prep, alpha, stream_),
-             "LaunchPrepare");
-    send = recv;
-  }
-  if (premul) {
+  if ((prep != kPrepCopy && !premul) || !RcclOp(op, &o)) {
+    // ops RCCL cannot express (BitOR) and prepares it cannot fuse (g*g, |g|): reduce-scatter
+    // by grouped point-to-point copies, our reduce kernel applying the prepare as it loads
+    // each rank's segment (no separate prepare pass), then the allgather
+    const int p = premul ? kPrepCopy : prep;
+    PassFn pass = [dtype, op, p, alpha](void *dst, const void *const *srcs, int n, size_t c,
+                                        bool acc_first, hipStream_t st) {
+      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, nullptr, nullptr, 0.0, nullptr, p,
+                               alpha, acc_first ? 1 : 0);
+    };
+    Status s = AllreduceByKernel(send, recv, count, TypeBytes(dtype), pass, probe);
+    if (s != Status::kSuccess) return s;
+  } else if (premul) {
     ncclRedOp_t pm;
     double a64 = alpha;
     float a32 = static_cast<float>(alpha);
@@ -630,20 +868,20 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
       a16 = bf16_t::FromFloat(a32);
       scalar = &a16;
     }
-    CheckNccl(ncclRedOpCreatePreMulSum(&pm, scalar, t, ncclScalarHostImmediate, comm_),
-              "ncclRedOpCreatePreMulSum");
-    CheckNccl(ncclAllReduce(send, recv, count, t, pm, comm_, stream_), "ncclAllReduce");
-    CheckNccl(ncclRedOpDestroy(pm, comm_), "ncclRedOpDestroy");
-  } else if (!RcclOp(op, &o)) {
-    PeerGroup::ReduceStep step = [dtype, op](void *dst, const void *const *srcs, int n, size_t c,
-                                             const int *guard, const void *const *table,
-                                             double post, hipStream_t st) {
-      return LaunchReduceMulti(dst, srcs, n, c, dtype, op, st, guard, table, post);
-    };
-    Status s = AllreduceByKernel(send, recv, count, TypeBytes(dtype), step, probe);
+    Status s = Rccl(ncclRedOpCreatePreMulSum(&pm, scalar, t, ncclScalarHostImmediate, comm_),
+                    "ncclRedOpCreatePreMulSum", probe);
+    if (s != Status::kSuccess) return s;
+    s = Rccl(MockRcclFault() ? ncclRemoteError
+                             : ncclAllReduce(send, recv, count, t, pm, comm_, stream_),
+             "ncclAllReduce", probe);
+    if (s != Status::kSuccess) return s;  // the aborted communicator took the op with it
+    s = Rccl(ncclRedOpDestroy(pm, comm_), "ncclRedOpDestroy", probe);
     if (s != Status::kSuccess) return s;
   } else {
-    CheckNccl(ncclAllReduce(send, recv, count, t, o, comm_, stream_), "ncclAllReduce");
+    Status s = Rccl(MockRcclFault() ? ncclRemoteError
+                                    : ncclAllReduce(send, recv, count, t, o, comm_, stream_),
+                    "ncclAllReduce", probe);
+    if (s != Status::kSuccess) return s;
   }
   // RCCL writes recv only; the second copy is enqueued by Finish once the op is known to have
   // succeeded (an aborted RCCL kernel leaves garbage in recv)
@@ -662,25 +900,40 @@ int DevicePlane::GraphAllreduce(void *buf, size_t count, int dtype, int op, hipS
   if (!RcclType(dtype, &t) || !RcclOp(op, &o)) return -3;
   if (count == 0) return 0;
   DeviceGuard dg(device_);
-  return ncclAllReduce(buf, buf, count, t, o, comm_, stream) == ncclSuccess ? 0 : -5;
+  rccl_calls_ += 1;
+  ncclResult_t r = ncclAllReduce(buf, buf, count, t, o, comm_, stream);
+  if (r == ncclInProgress) {
+    // non-blocking communicator: the enqueue completes on RCCL's side (host-side polling only,
+    // so this is legal while `stream` is being captured)
+    ncclResult_t st = ncclInProgress;
+    while (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st == ncclInProgress) {
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    r = st;
+  }
+  return r == ncclSuccess ? 0 : -5;
 }
 
 Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                                     size_t type_nbytes, DeviceReduceLauncher *launcher,
                                     const FailureProbe &probe) {
-  PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
-                                          const int *guard, const void *const *, double,
-                                          hipStream_t st) {
-    return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
-  };
   const size_t bytes = count * type_nbytes;
   op_bytes_ = bytes;
   if (UseDirect(bytes)) {
+    PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
+                                            const int *guard, const void *const *, double,
+                                            hipStream_t st) {
+      return static_cast<hipError_t>(launcher(dst, srcs, n, c, guard, st));
+    };
     CheckHip(peers_->AllreduceCustom(send, recv, recv2, count, type_nbytes, step),
              "direct allreduce (custom)");
     return Status::kSuccess;
   }
-  Status s = AllreduceByKernel(send, recv, count, type_nbytes, step, probe);
+  PassFn pass = [launcher](void *dst, const void *const *srcs, int n, size_t c, bool,
+                           hipStream_t st) {
+    return static_cast<hipError_t>(launcher(dst, srcs, n, c, nullptr, st));
+  };
+  Status s = AllreduceByKernel(send, recv, count, type_nbytes, pass, probe);
   if (s != Status::kSuccess) return s;
   if (recv2 != nullptr && recv2 != recv) {
     pending_dst_ = recv2;
@@ -691,85 +944,59 @@ Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, s
 }
 
 Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count, size_t tn,
-                                      const PeerGroup::ReduceStep &step,
-                                      const FailureProbe &probe) {
-  (void)probe;
+                                      const PassFn &pass, const FailureProbe &probe) {
   utils::Check(comm_ != nullptr, "device allreduce without communicator");
-  const int n = nranks_;
   // reduce-scatter + allgather as two rounds of grouped point-to-point copies that read and
-  // write the buffers in place (segments are whole 256-element blocks, so every segment start
-  // is as aligned as the buffer): no packing into scratch, no unpacking afterwards
-  const size_t seg = ((count + n - 1) / n + 255) / 256 * 256;
-  auto lo = [&](int k) { return std::min(count, seg * static_cast<size_t>(k)); };
-  auto hi = [&](int k) { return std::min(count, seg * static_cast<size_t>(k + 1)); };
+  // write the buffers in place (p2p_plan.h: segments are whole 256-element blocks, so every
+  // segment start is as aligned as the buffer): no packing into scratch, no unpacking
+  const SegmentPlan plan(count, tn, nranks_);
   const char *in = static_cast<const char *>(send);
   char *out = static_cast<char *>(recv);
-  const size_t mine = hi(rank_) - lo(rank_);
-  const size_t slot = (mine * tn + 255) / 256 * 256;
-  char *inbox = static_cast<char *>(Scratch(std::max<size_t>(slot * n, 256), 1));
+  char *inbox = static_cast<char *>(Scratch(plan.inbox_bytes(rank_), 1));
+  char *bufs[3] = {const_cast<char *>(in), out, inbox};
+  auto at = [&bufs](size_t, const P2POp &o) { return bufs[o.buf] + o.offset; };
   // 1. segment k of every rank's input goes to rank k
-  CheckNccl(ncclGroupStart(), "ncclGroupStart");
-  for (int k = 0; k < n; ++k) {
-    if (k == rank_) continue;
-    if (hi(k) > lo(k)) {
-      CheckNccl(ncclSend(in + lo(k) * tn, (hi(k) - lo(k)) * tn, ncclUint8, k, comm_, stream_),
-                "ncclSend");
-    }
-    if (mine != 0) {
-      CheckNccl(ncclRecv(inbox + static_cast<size_t>(k) * slot, mine * tn, ncclUint8, k, comm_,
-                         stream_),
-                "ncclRecv");
-    }
-  }
-  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+  Status s = RunP2P(plan.ScatterOps(rank_), at, "allreduce reduce-scatter", probe);
+  if (s != Status::kSuccess) return s;
   // 2. reduce the n copies of my segment (rank order, up to 8 sources per pass) into place
-  if (mine != 0) {
-    std::vector<const void *> srcs;
-    int done = 0;
-    char *dst = out + lo(rank_) * tn;
-    while (done < n) {
-      srcs.clear();
-      if (done > 0) srcs.push_back(dst);
-      while (done < n && static_cast<int>(srcs.size()) < kMaxReduceSources) {
-        srcs.push_back(done == rank_ ? static_cast<const void *>(in + lo(rank_) * tn)
-                                     : inbox + static_cast<size_t>(done) * slot);
-        ++done;
-      }
-      CheckHip(step(dst, srcs.data(), static_cast<int>(srcs.size()), mine, nullptr, nullptr, 0.0,
-                    stream_),
-               "allreduce reduce step");
+  char *dst = out + plan.lo(rank_) * tn;
+  std::vector<const void *> srcs;
+  for (const std::vector<int> &p : plan.ReducePasses(rank_, kMaxReduceSources)) {
+    srcs.clear();
+    for (int k : p) {
+      srcs.push_back(k < 0 ? static_cast<const void *>(dst)
+                           : (k == rank_ ? static_cast<const void *>(in + plan.lo(rank_) * tn)
+                                         : inbox + static_cast<size_t>(k) * plan.slot_bytes(rank_)));
     }
+    CheckHip(pass(dst, srcs.data(), static_cast<int>(srcs.size()), plan.elems(rank_), p[0] < 0,
+                  stream_),
+             "allreduce reduce step");
   }
   // 3. every reduced segment to every rank, straight into its place in recv
-  CheckNccl(ncclGroupStart(), "ncclGroupStart");
-  for (int k = 0; k < n; ++k) {
-    if (k == rank_) continue;
-    if (mine != 0) {
-      CheckNccl(ncclSend(out + lo(rank_) * tn, mine * tn, ncclUint8, k, comm_, stream_),
-                "ncclSend");
-    }
-    if (hi(k) > lo(k)) {
-      CheckNccl(ncclRecv(out + lo(k) * tn, (hi(k) - lo(k)) * tn, ncclUint8, k, comm_, stream_),
-                "ncclRecv");
-    }
-  }
-  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
-  return Status::kSuccess;
+  return RunP2P(plan.GatherOps(rank_), at, "allreduce allgather", probe);
 }
 
-Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe) {
-  (void)probe;
+Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe,
+                              void *log) {
   op_bytes_ = bytes;
   if (UseDirect(bytes)) {
-    CheckHip(peers_->Broadcast(buf, bytes, root), "direct broadcast");
+    CheckHip(peers_->Broadcast(buf, bytes, root, log), "direct broadcast");
     return Status::kSuccess;
   }
   utils::Check(comm_ != nullptr, "device broadcast without communicator");
-  CheckNccl(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
-  return Status::kSuccess;
+  Status s = Rccl(MockRcclFault() ? ncclRemoteError
+                                  : ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_),
+                  "ncclBroadcast", probe);
+  if (s == Status::kSuccess && log != nullptr && log != buf) {
+    pending_dst_ = log;  // copied by Finish once the op is known to have succeeded
+    pending_src_ = buf;
+    pending_bytes_ = bytes;
+  }
+  return s;
 }
 
-Status DevicePlane::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in) {
+Status DevicePlane::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in,
+                             const FailureProbe &probe) {
   *bytes_in = 0;
   op_bytes_ = 0;
   for (const ExchangeItem &x : plan) op_bytes_ += x.bytes;
@@ -778,65 +1005,61 @@ Status DevicePlane::Exchange(const std::vector<ExchangeItem> &plan, size_t *byte
     CheckHip(peers_->Exchange(plan, bytes_in), "direct exchange");
     return Status::kSuccess;
   }
-  // a copy to itself is a local kernel; the rest pairs up as ncclSend / ncclRecv
-  bool any = false;
-  for (const ExchangeItem &x : plan) {
-    if (x.bytes == 0) continue;
-    if (x.src == rank_ && x.dst == rank_) {
-      CopyDeviceAsync(x.dst_ptr, x.src_ptr, x.bytes);
-    } else if (x.src == rank_ || x.dst == rank_) {
-      any = true;
-    }
-  }
-  if (!any) return Status::kSuccess;
+  // a copy to itself is a local kernel; the rest pairs up as ncclSend / ncclRecv (p2p_plan.h:
+  // every rank walks the same plan in the same order, so the k-th send from s to d meets the
+  // k-th receive at d from s)
+  std::vector<size_t> item_of, local;
+  const std::vector<P2POp> ops = ExchangeOps(plan, rank_, &item_of, &local);
+  for (size_t i : local) CopyDeviceAsync(plan[i].dst_ptr, plan[i].src_ptr, plan[i].bytes);
+  if (ops.empty()) return Status::kSuccess;
   utils::Check(comm_ != nullptr, "device exchange without a transport");
-  CheckNccl(ncclGroupStart(), "ncclGroupStart");
-  for (const ExchangeItem &x : plan) {
-    if (x.bytes == 0 || x.src == x.dst) continue;
-    if (x.src == rank_) {
-      CheckNccl(ncclSend(x.src_ptr, x.bytes, ncclUint8, x.dst, comm_, stream_), "ncclSend");
-    } else if (x.dst == rank_) {
-      CheckNccl(ncclRecv(x.dst_ptr, x.bytes, ncclUint8, x.src, comm_, stream_), "ncclRecv");
-      *bytes_in += x.bytes;
-    }
+  for (const P2POp &o : ops) {
+    if (!o.send) *bytes_in += o.bytes;
   }
-  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
-  return Status::kSuccess;
+  auto at = [&plan, &item_of](size_t i, const P2POp &o) {
+    const ExchangeItem &x = plan[item_of[i]];
+    return o.send ? static_cast<char *>(const_cast<void *>(x.src_ptr))
+                  : static_cast<char *>(x.dst_ptr);
+  };
+  return RunP2P(ops, at, "exchange", probe);
 }
 
 Status DevicePlane::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
-                               const std::vector<size_t> &size, const FailureProbe &probe) {
-  (void)probe;
+                               const std::vector<size_t> &size, const FailureProbe &probe,
+                               void *log) {
   op_bytes_ = total;
   if (UseDirect(total)) {
-    CheckHip(peers_->AllgatherV(buf_, total, begin, size), "direct allgather");
+    CheckHip(peers_->AllgatherV(buf_, total, begin, size, log), "direct allgather");
     return Status::kSuccess;
   }
   utils::Check(comm_ != nullptr, "device allgather without communicator");
   char *buf = static_cast<char *>(buf_);
-  const int n = nranks_;
-  bool uniform = total == size[0] * n;
-  for (int r = 0; r < n && uniform; ++r) uniform = begin[r] == r * size[0] && size[r] == size[0];
-  if (uniform) {
-    CheckNccl(ncclAllGather(buf + begin[rank_], buf, size[0], ncclUint8, comm_, stream_),
-              "ncclAllGather");
-    return Status::kSuccess;
-  }
-  CheckNccl(ncclGroupStart(), "ncclGroupStart");
-  for (int r = 0; r < n; ++r) {
-    size_t b = begin[r] % total, s = size[r];
-    const size_t first = std::min(s, total - b);
-    if (first != 0) {
-      CheckNccl(ncclBroadcast(buf + b, buf + b, first, ncclUint8, r, comm_, stream_),
-                "ncclBroadcast");
+  Status s;
+  if (AllgatherUniform(total, begin, size)) {
+    s = Rccl(MockRcclFault() ? ncclRemoteError
+                             : ncclAllGather(buf + begin[rank_], buf, size[0], ncclUint8, comm_,
+                                             stream_),
+             "ncclAllGather", probe);
+  } else if (MockRcclFault()) {
+    s = FailRccl("allgather", ncclRemoteError);
+  } else {
+    // variable, wrapping slices: one broadcast per piece (p2p_plan.h), in one group
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return Rccl(r, "allgather", probe);
+    for (const BcastPiece &p : AllgatherPieces(total, begin, size)) {
+      if (r != ncclSuccess) break;
+      r = ncclBroadcast(buf + p.offset, buf + p.offset, p.bytes, ncclUint8, p.root, comm_,
+                        stream_);
     }
-    if (s > first) {
-      CheckNccl(ncclBroadcast(buf, buf, s - first, ncclUint8, r, comm_, stream_),
-                "ncclBroadcast");
-    }
+    const ncclResult_t e = ncclGroupEnd();
+    s = Rccl(r != ncclSuccess ? r : e, "allgather", probe);
   }
-  CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
-  return Status::kSuccess;
+  if (s == Status::kSuccess && log != nullptr && log != buf) {
+    pending_dst_ = log;
+    pending_src_ = buf;
+    pending_bytes_ = total;
+  }
+  return s;
 }
 }  // namespace device
 }  // namespace rabit

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "device/p2p_plan.h"
 #include "device/peer_coll.h"
 #include "net/socket.h"
 
@@ -66,6 +67,13 @@ struct DeviceConfig {
   size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
   int rccl_max_ctas{0};
+  // RCCL communicator lifecycle: the bring-up (init and the connection
+  // of every channel) runs on a helper thread watched by the failure probe and a deadline, so
+  // a peer that dies mid-init costs kAborted / kTimeout instead of a hang (see InitComm)
+  double comm_init_timeout_sec{120};   // deadline of communicator bring-up (0: none)
+  int rccl_max_failures{8};            // consecutive aborted RCCL ops before the error is fatal
+  int mock_rccl_error{0};              // test hook: the n-th RCCL enqueue (1-based) fails with
+                                       // ncclRemoteError instead of running
 };
 
 /*! \brief exit status of a rank whose own device stream stayed wedged after an abort (the
@@ -162,7 +170,12 @@ class DevicePlane {
   // ---- communicator lifecycle
   /*! \brief serialized ncclUniqueId (NCCL_UNIQUE_ID_BYTES bytes) */
   static std::string NewUniqueId();
-  /*! \brief collective over all ranks: build the communicator of a new epoch */
+  /*!
+   * \brief collective over all ranks: build the communicator of a new epoch and connect all
+   *        its channels, on a helper thread, while this thread watches `probe` and
+   *        comm_init_timeout_sec: a rank that never joins (or dies during the bring-up) costs the
+   *        others kAborted / kTimeout, not a hang.
+   */
   Status InitComm(const std::string &id, int nranks, int rank, const FailureProbe &probe);
   /*! \brief abort the communicator and the peer group (unblocks in-flight kernels), drop them */
   void AbortComm();
@@ -294,17 +307,24 @@ class DevicePlane {
   Status AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                          size_t type_nbytes, DeviceReduceLauncher *launcher,
                          const FailureProbe &probe);
-  Status Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe);
-  /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place */
+  /*! \brief in-place broadcast; log != nullptr: the result is also stored there once the op
+   *  succeeded (the direct transport's kernels store it in the same pass, RCCL by a copy that
+   *  Finish enqueues) */
+  Status Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe,
+                   void *log = nullptr);
+  /*! \brief rabit Allgather: slice r = [begin[r], begin[r]+size[r]) mod total, in place
+   *  (log: as for Broadcast) */
   Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
-                    const std::vector<size_t> &size, const FailureProbe &probe);
+                    const std::vector<size_t> &size, const FailureProbe &probe,
+                    void *log = nullptr);
   /*!
    * \brief point-to-point copies over xGMI (see ExchangeItem; every rank passes the same plan).
    *        With RCCL: one grouped ncclSend/ncclRecv call on the ranks that take part (the others
    *        do nothing); otherwise the direct transport's stage exchange.  Enqueue only: the
    *        caller waits with Finish().  *bytes_in: payload bytes this rank received from peers.
    */
-  Status Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in);
+  Status Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in,
+                  const FailureProbe &probe = FailureProbe());
   /*! \brief stage a host-reducer allreduce through pinned host memory */
   void StageToHost(void *host, const void *dev, size_t bytes);
   void StageToDevice(void *dev, const void *host, size_t bytes);
@@ -343,10 +363,44 @@ class DevicePlane {
   /*! \brief reusable scratch buffer of at least bytes */
   void *Scratch(size_t bytes, int slot = 0);
 
+  /*! \brief RCCL enqueue calls made so far, and the ones that returned ncclInProgress and were
+   *  settled by polling (non-blocking communicator) */
+  uint64_t rccl_calls() const { return rccl_calls_; }
+  uint64_t rccl_settled() const { return rccl_settled_; }
+  /*! \brief RCCL results turned into kAborted / kTimeout (the engine recovered) */
+  uint64_t rccl_aborts() const { return rccl_aborts_; }
+  /*! \brief communicator bring-ups given up while RCCL's bootstrap still waited on a peer */
+  uint64_t init_abandoned() const { return init_abandoned_; }
+
  private:
   Status WaitEvent(hipEvent_t ev, const FailureProbe &probe);
+  /*!
+   * \brief map an RCCL return code to a Status: success; ncclInProgress (non-blocking
+   *        communicator) is polled to completion under the probe and the op deadline; a result a
+   *        dead peer can cause aborts the communicator and returns kAborted (the engine
+   *        recovers); a usage error is fatal
+   */
+  Status Rccl(int result, const char *what, const FailureProbe &probe);
+  /*! \brief poll ncclCommGetAsyncError until the communicator leaves ncclInProgress; abort it on
+   *  an error, a peer failure or after limit_sec (> 0) */
+  Status Settle(const char *what, const FailureProbe &probe, double limit_sec);
+  /*! \brief abort the communicator after a failed RCCL call (kAborted), or throw if the call
+   *  cannot have failed because of a peer */
+  Status FailRccl(const char *what, int result);
+  /*! \brief count one RCCL enqueue; true when the mock_rccl_error hook makes it fail */
+  bool MockRcclFault();
+  /*! \brief one grouped ncclSend / ncclRecv call over ops (pointers from at(i, op)) */
+  Status RunP2P(const std::vector<P2POp> &ops, const std::function<char *(size_t, const P2POp &)> &at,
+                const char *what, const FailureProbe &probe);
+  /*! \brief one reduce pass of the kernel-reduced allreduce: dst = reduce(srcs) over count
+   *  elements; acc_first: srcs[0] is the running result of an earlier pass (not prepared) */
+  typedef std::function<hipError_t(void *dst, const void *const *srcs, int nsrc, size_t count,
+                                   bool acc_first, hipStream_t stream)>
+      PassFn;
+  /*! \brief RCCL allreduce for what ncclAllReduce cannot do (BitOR, custom and prepared
+   *  reductions): grouped p2p reduce-scatter (SegmentPlan), `pass`, grouped p2p allgather */
   Status AllreduceByKernel(const void *send, void *recv, size_t count, size_t type_nbytes,
-                           const PeerGroup::ReduceStep &step, const FailureProbe &probe);
+                           const PassFn &pass, const FailureProbe &probe);
 
   DeviceConfig cfg_;
   int device_{-1};
@@ -376,6 +430,9 @@ class DevicePlane {
   size_t pinned_bytes_{0};
   size_t op_bytes_{0};
   std::vector<PeerLinkInfo> links_;
+  uint64_t rccl_calls_{0}, rccl_settled_{0}, rccl_aborts_{0}, init_abandoned_{0};
+  void *warm_{nullptr};  // 4 KiB of HBM for the bring-up's connection warm-up
+  int rccl_fail_streak_{0};  // aborted RCCL ops since the last op that completed
 };
 
 /*! \brief throw rabit::Error on a HIP failure */

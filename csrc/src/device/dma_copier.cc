@@ -7,6 +7,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <algorithm>
 #include <cstdio>
 
 #include "device/device_plane.h"
@@ -101,24 +102,37 @@ bool DmaCopier::Done(uint64_t ticket) const {
   return completed_ >= ticket;
 }
 
-void DmaCopier::Wait(uint64_t ticket) {
+bool DmaCopier::Wait(uint64_t ticket) {
   std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&]() { return completed_ >= ticket || failed_; });
-  utils::Check(!failed_, "SDMA mirror copy failed");
+  done_cv_.wait(lk, [&]() { return completed_ >= ticket; });
+  // a mirror is several jobs (one per buffer) and is waited for by its last ticket: any
+  // unreported failure up to it counts (an older one only costs a redundant redo)
+  const size_t before = failed_.size();
+  failed_.erase(std::remove_if(failed_.begin(), failed_.end(),
+                               [ticket](uint64_t t) { return t <= ticket; }),
+                failed_.end());
+  return failed_.size() == before;
 }
 
-void DmaCopier::WaitAll() {
-  uint64_t last;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    last = submitted_;
-  }
-  Wait(last);
+bool DmaCopier::WaitAll() {
+  std::unique_lock<std::mutex> lk(mu_);
+  const uint64_t last = submitted_;
+  done_cv_.wait(lk, [&]() { return completed_ >= last; });
+  const bool ok = failed_.empty();
+  failed_.clear();
+  return ok;
 }
 
 void DmaCopier::Run() {
   hsa_signal_t sig;
   const bool have_sig = hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS;
+  // fallback for a copy the SDMA path refused or failed: the same bytes by hipMemcpyAsync on a
+  // stream of this thread (a blit kernel; slower for the caller's kernels, but the mirror lands)
+  hipStream_t fallback = nullptr;
+  if (hipStreamCreateWithFlags(&fallback, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    fallback = nullptr;
+  }
   hsa_agent_t gpu{gpu_agent_}, cpu{cpu_agent_};
   // the first engine ROCr reports free for this direction (engine 0 if it cannot say)
   uint32_t mask = 0;
@@ -135,7 +149,8 @@ void DmaCopier::Run() {
       job = jobs_.front();
       jobs_.pop_front();
     }
-    bool ok = have_sig && hipEventSynchronize(job.ready) == hipSuccess;
+    const bool ready = hipEventSynchronize(job.ready) == hipSuccess;
+    bool ok = have_sig && ready;
     if (ok && job.bytes != 0) {
       hsa_signal_store_relaxed(sig, 1);
       hsa_status_t st = hsa_amd_memory_async_copy_on_engine(job.dst, cpu, job.src, gpu, job.bytes,
@@ -148,13 +163,23 @@ void DmaCopier::Run() {
            hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
                                      HSA_WAIT_STATE_BLOCKED) == 0;
     }
+    if (!ok && ready && job.bytes != 0 && fallback != nullptr) {
+      if (fallbacks_.fetch_add(1) == 0) {
+        utils::HandleLogInfo("[xrabit] SDMA mirror copy failed: copying with hipMemcpyAsync\n");
+      }
+      ok = hipMemcpyAsync(job.dst, job.src, job.bytes, hipMemcpyDeviceToHost, fallback) ==
+               hipSuccess &&
+           hipStreamSynchronize(fallback) == hipSuccess;
+      if (!ok) (void)hipGetLastError();
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (!ok) failed_ = true;
+      if (!ok) failed_.push_back(job.ticket);
       completed_ = job.ticket;
     }
     done_cv_.notify_all();
   }
+  if (fallback != nullptr) (void)hipStreamDestroy(fallback);
   if (have_sig) hsa_signal_destroy(sig);
 }
 

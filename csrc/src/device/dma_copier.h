@@ -19,12 +19,14 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 
 namespace rabit {
 namespace device {
@@ -41,12 +43,19 @@ class DmaCopier {
    *        ticket (tickets grow by one per job, 0 is "nothing")
    */
   uint64_t Submit(void *dst, const void *src, size_t bytes, hipEvent_t ready);
-  /*! \brief the job with this ticket (and every earlier one) has finished */
+  /*! \brief the job with this ticket (and every earlier one) has finished (copied or failed) */
   bool Done(uint64_t ticket) const;
-  /*! \brief block until the job with this ticket has finished; fails loudly if a copy failed */
-  void Wait(uint64_t ticket);
-  /*! \brief block until every queued job has finished */
-  void WaitAll();
+  /*!
+   * \brief block until the job with this ticket has finished; false if its bytes did not land
+   *        (the SDMA copy and the worker's hipMemcpyAsync fallback both failed), in which case
+   *        the caller redoes the copy another way.  Any unreported failure of a job up to this
+   *        ticket counts, and is reported once.
+   */
+  bool Wait(uint64_t ticket);
+  /*! \brief block until every queued job has finished; false if any of them failed (never
+   *  throws: also called from destructors) */
+  bool WaitAll();
+  uint64_t fallbacks() const { return fallbacks_.load(); }
 
  private:
   struct Job {
@@ -66,7 +75,8 @@ class DmaCopier {
   std::deque<Job> jobs_;
   uint64_t submitted_{0};
   uint64_t completed_{0};
-  bool failed_{false};
+  std::vector<uint64_t> failed_;   // tickets whose copy failed, not yet reported by Wait
+  std::atomic<uint64_t> fallbacks_{0};
   bool stop_{false};
   std::thread worker_;
 };

@@ -209,6 +209,93 @@ __device__ __forceinline__ void PutVec(T *dst, size_t e, uint4 v, bool vec) {
   }
 }
 
+/*!
+ * \brief reduce phase of one tile: res / out / out2 [v] = op over the n sources s_in[k][v] for
+ *        the nvec 16-byte vectors of the tile.  Each lane loads U vectors of every source before
+ *        it combines or stores any (MAXN x U x 16 B in flight per lane; MAXN x U <= 16 keeps the
+ *        4-workgroups-per-CU register budget), sources in rank order.
+ */
+template <typename T, int OP, int MAXN, int U>
+__device__ __forceinline__ void ReduceTileVec(const char *const *s_in, int n, size_t nvec, T *out,
+                                              T *out2, uint4 *res, size_t lo, bool vout,
+                                              double post) {
+  constexpr size_t L = 16 / sizeof(T);
+  size_t v = threadIdx.x;
+  for (; v + (U - 1) * kBlock < nvec; v += U * kBlock) {
+    uint4 x[U][MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) {
+      if (k < n) {
+        const uint4 *sk = reinterpret_cast<const uint4 *>(s_in[k]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u][k] = sk[v + u * kBlock];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 y = ReduceVecsN<T, OP, MAXN>(x[u], n, post);
+      const size_t e = lo + (v + u * kBlock) * L;
+      PutVec<T>(out, e, y, vout);
+      if (out2 != nullptr) PutVec<T>(out2, e, y, vout);
+      res[v + u * kBlock] = y;
+    }
+  }
+  for (; v < nvec; v += kBlock) {
+    uint4 x[MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) {
+      if (k < n) x[k] = reinterpret_cast<const uint4 *>(s_in[k])[v];
+    }
+    const uint4 y = ReduceVecsN<T, OP, MAXN>(x, n, post);
+    PutVec<T>(out, lo + v * L, y, vout);
+    if (out2 != nullptr) PutVec<T>(out2, lo + v * L, y, vout);
+    res[v] = y;
+  }
+}
+
+/*!
+ * \brief gather phase of one tile index: copy the reduced tile of every other rank p (s_nv[p]
+ *        elements at s_lo[p] of its stage; 0 for this rank) into out / out2, U vectors per peer
+ *        per lane loaded before any store (whole 16-byte vectors; the element tails follow in
+ *        the caller)
+ */
+template <typename T, int MAXN, int U>
+__device__ __forceinline__ void GatherTileVec(const FusedAllreduceArgs &a, const size_t *s_lo,
+                                              const size_t *s_nv, int n, T *out, T *out2,
+                                              bool vout) {
+  constexpr size_t L = 16 / sizeof(T);
+  const size_t most = (a.tile + L - 1) / L;
+  for (size_t v = threadIdx.x; v < most; v += U * kBlock) {
+    uint4 x[U][MAXN];
+#pragma unroll
+    for (int p = 0; p < MAXN; ++p) {
+      if (p < n) {
+        const size_t nv = s_nv[p] / L;
+        const uint4 *sp =
+            reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(a.stage[p]) + s_lo[p]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (v + u * kBlock < nv) x[u][p] = sp[v + u * kBlock];
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < MAXN; ++p) {
+      if (p < n) {
+        const size_t nv = s_nv[p] / L;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const size_t w = v + u * kBlock;
+          if (w < nv) {
+            PutVec<T>(out, s_lo[p] + w * L, x[u][p], vout);
+            if (out2 != nullptr) PutVec<T>(out2, s_lo[p] + w * L, x[u][p], vout);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduceArgs a) {
   __shared__ int s_bad;
@@ -291,17 +378,12 @@ __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduce
     if (hi > lo) {
       const size_t nvec = (hi - lo) / L;
       uint4 *res = reinterpret_cast<uint4 *>(mine + lo);
-      for (size_t v = threadIdx.x; v < nvec; v += kBlock) {
-        uint4 x[kMaxPeers];
-#pragma unroll
-        for (int k = 0; k < kMaxPeers; ++k) {
-          if (k < n) x[k] = reinterpret_cast<const uint4 *>(s_in[k])[v];
-        }
-        const uint4 y = ReduceVecsN<T, OP, kMaxPeers>(x, n, a.post);
-        const size_t e = lo + v * L;
-        PutVec<T>(out, e, y, vout);
-        if (out2 != nullptr) PutVec<T>(out2, e, y, vout);
-        res[v] = y;
+      // U vectors per lane per step, every load of the step issued before any store: with one
+      // load per source in flight a lane waited a full (remote) latency per 16 bytes
+      if (n <= 4) {
+        ReduceTileVec<T, OP, 4, 4>(s_in, n, nvec, out, out2, res, lo, vout, a.post);
+      } else {
+        ReduceTileVec<T, OP, kMaxPeers, 2>(s_in, n, nvec, out, out2, res, lo, vout, a.post);
       }
       for (size_t e = nvec * L + threadIdx.x; e < hi - lo; e += kBlock) {
         const T *srcs[kMaxPeers];
@@ -329,23 +411,10 @@ __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduce
       s_nv[p] = hi - lo;  // elements
     }
     __syncthreads();
-    const size_t most = (a.tile + L - 1) / L;
-    for (size_t v = threadIdx.x; v < most; v += kBlock) {
-      uint4 x[kMaxPeers];
-#pragma unroll
-      for (int p = 0; p < kMaxPeers; ++p) {
-        if (p < n && (v + 1) * L <= s_nv[p]) {
-          x[p] = reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(a.stage[p]) +
-                                                 s_lo[p])[v];
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < kMaxPeers; ++p) {
-        if (p < n && (v + 1) * L <= s_nv[p]) {
-          PutVec<T>(out, s_lo[p] + v * L, x[p], vout);
-          if (out2 != nullptr) PutVec<T>(out2, s_lo[p] + v * L, x[p], vout);
-        }
-      }
+    if (n <= 4) {
+      GatherTileVec<T, 4, 4>(a, s_lo, s_nv, n, out, out2, vout);
+    } else {
+      GatherTileVec<T, kMaxPeers, 2>(a, s_lo, s_nv, n, out, out2, vout);
     }
     for (int p = 0; p < n; ++p) {
       const size_t nel = s_nv[p];

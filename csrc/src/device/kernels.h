@@ -37,10 +37,16 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
  *        dst2: optional second destination written with the same values by the same kernel
  *        (the user buffer next to the result log: one launch and one read instead of two).
  */
+/*!
+ *        prep != kPrepCopy: the lazy prepare (g*g, alpha*g, |g|) is applied to sources
+ *        prep_from..nsrc-1 as they are loaded (the running result of an earlier pass sits at
+ *        index 0 with prep_from = 1), so a prepared allreduce needs no pass of its own.
+ */
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard = nullptr,
                              const void *const *table = nullptr, double post_scale = 0.0,
-                             void *dst2 = nullptr);
+                             void *dst2 = nullptr, int prep = 0, double prep_alpha = 1.0,
+                             int prep_from = 0);
 /*! \brief dst[i] = prep(src[i]); also dst2[i] when dst2 != nullptr */
 hipError_t LaunchPrepare(void *dst, void *dst2, const void *src, size_t count, int dtype,
                          int prep, double alpha, hipStream_t stream);

@@ -112,6 +112,9 @@ struct SrcList {
   const void *const *table;  // optional: device table of source pointers (overrides p)
   double post_scale;         // != 0: multiply the reduced value by it (floating types)
   void *dst2;                // optional second destination (same values as dst)
+  int prep;                  // PrepOp applied to sources prep_from.. as they are loaded (the
+  int prep_from;             // lazy prepare fused into the reduce: no separate pass)
+  double prep_alpha;
 };
 
 /*! \brief source k: from the device table when given (written by an earlier kernel, e.g. a
@@ -126,18 +129,24 @@ __device__ __forceinline__ bool Guarded(const int *guard) {
 }
 
 /*! \brief scalar form of ReduceVecs over nsrc sources (tails, unaligned buffers) */
+template <typename T>
+__device__ __forceinline__ T LoadSrc(const SrcList &srcs, int k, size_t i) {
+  const T x = static_cast<const T *>(Src(srcs, k))[i];
+  return srcs.prep != 0 && k >= srcs.prep_from
+             ? PrepApply<T>(x, srcs.prep, static_cast<T>(srcs.prep_alpha))
+             : x;
+}
+
 template <typename T, int OP>
 __device__ __forceinline__ T ReduceScalar(const SrcList &srcs, int nsrc, size_t i) {
   if constexpr (IsHalfType<T>::value) {
-    float acc = static_cast<const T *>(Src(srcs, 0))[i].f();
-    for (int k = 1; k < nsrc; ++k) {
-      acc = Apply<float, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i].f());
-    }
+    float acc = LoadSrc<T>(srcs, 0, i).f();
+    for (int k = 1; k < nsrc; ++k) acc = Apply<float, OP>::f(acc, LoadSrc<T>(srcs, k, i).f());
     if (srcs.post_scale != 0.0) acc *= static_cast<float>(srcs.post_scale);
     return T(acc);
   } else {
-    T acc = static_cast<const T *>(Src(srcs, 0))[i];
-    for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, static_cast<const T *>(Src(srcs, k))[i]);
+    T acc = LoadSrc<T>(srcs, 0, i);
+    for (int k = 1; k < nsrc; ++k) acc = Apply<T, OP>::f(acc, LoadSrc<T>(srcs, k, i));
     if (srcs.post_scale != 0.0) acc = acc * static_cast<T>(srcs.post_scale);
     return acc;
   }
@@ -157,6 +166,14 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
 #pragma unroll
       for (int u = 0; u < U; ++u) x[k][u] = reinterpret_cast<const uint4 *>(Src(srcs, k))[base + u * kBlock];
     }
+    if (srcs.prep != 0) {  // uniform branch: the fused lazy prepare, applied on load
+#pragma unroll
+      for (int k = 0; k < NSRC; ++k) {
+        if (k < srcs.prep_from) continue;
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[k][u] = PrepVec<T>(x[k][u], srcs.prep, static_cast<T>(srcs.prep_alpha));
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       uint4 v[NSRC];
@@ -172,7 +189,12 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       if (i >= nvec) break;
       uint4 v[NSRC];
 #pragma unroll
-      for (int k = 0; k < NSRC; ++k) v[k] = reinterpret_cast<const uint4 *>(Src(srcs, k))[i];
+      for (int k = 0; k < NSRC; ++k) {
+        v[k] = reinterpret_cast<const uint4 *>(Src(srcs, k))[i];
+        if (srcs.prep != 0 && k >= srcs.prep_from) {
+          v[k] = PrepVec<T>(v[k], srcs.prep, static_cast<T>(srcs.prep_alpha));
+        }
+      }
       const uint4 acc = ReduceVecs<T, OP, NSRC>(v, srcs.post_scale);
       StoreNT(d + i, acc);  // same store kind as the main path (merged stores keep nt)
       if (d2 != nullptr) StoreNT(d2 + i, acc);
@@ -206,12 +228,15 @@ void LaunchMultiTile(T *dst, const SrcList &sl, size_t n, hipStream_t st) {
 template <typename T, int OP>
 hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st,
                        const int *guard, const void *const *table, double post_scale,
-                       void *dst2) {
+                       void *dst2, int prep = 0, double prep_alpha = 1.0, int prep_from = 0) {
   SrcList sl;
   sl.guard = guard;
   sl.table = table;
   sl.post_scale = post_scale;
   sl.dst2 = dst2;
+  sl.prep = prep;
+  sl.prep_from = prep_from;
+  sl.prep_alpha = prep_alpha;
   bool aligned = Aligned16(dst) && (dst2 == nullptr || Aligned16(dst2));
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;
@@ -502,9 +527,10 @@ struct OrTag {
     return hipErrorInvalidValue;
   }
   static hipError_t MultiOr(void *d, const void *const *s, int k, size_t n, hipStream_t st,
-                            const int *guard, const void *const *table, void *d2) {
+                            const int *guard, const void *const *table, void *d2, int prep,
+                            double alpha, int prep_from) {
     if constexpr (std::is_integral<T>::value) {
-      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table, 0.0, d2);
+      return ReduceMulti<T, kOpOr>(d, s, k, n, st, guard, table, 0.0, d2, prep, alpha, prep_from);
     }
     return hipErrorInvalidValue;
   }
@@ -528,7 +554,8 @@ hipError_t LaunchReduce(void *dst, const void *src, size_t count, int dtype, int
 
 hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t count,
                              int dtype, int op, hipStream_t stream, const int *guard,
-                             const void *const *table, double post_scale, void *dst2) {
+                             const void *const *table, double post_scale, void *dst2, int prep,
+                             double prep_alpha, int prep_from) {
   if (count == 0) return hipSuccess;
   if (post_scale != 0.0 && dtype != 6 && dtype != 7 && dtype != 10 && dtype != 11) {
     return hipErrorInvalidValue;  // floating types only
@@ -538,12 +565,17 @@ hipError_t LaunchReduceMulti(void *dst, const void *const *srcs, int nsrc, size_
     using T = typename std::remove_pointer<decltype(tag)>::type;
     switch (op) {
       case kOpMax:
-        return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
+        return ReduceMulti<T, kOpMax>(dst, srcs, nsrc, count, stream, guard, table, post_scale,
+                                      dst2, prep, prep_alpha, prep_from);
       case kOpMin:
-        return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
+        return ReduceMulti<T, kOpMin>(dst, srcs, nsrc, count, stream, guard, table, post_scale,
+                                      dst2, prep, prep_alpha, prep_from);
       case kOpSum:
-        return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table, post_scale, dst2);
-      case kOpOr: return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table, dst2);
+        return ReduceMulti<T, kOpSum>(dst, srcs, nsrc, count, stream, guard, table, post_scale,
+                                      dst2, prep, prep_alpha, prep_from);
+      case kOpOr:
+        return OrTag<T>::MultiOr(dst, srcs, nsrc, count, stream, guard, table, dst2, prep,
+                                 prep_alpha, prep_from);
       default: return hipErrorInvalidValue;
     }
   });

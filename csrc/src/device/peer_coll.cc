@@ -524,32 +524,48 @@ void PeerGroup::CollectTiming() {
   ++timed_ops_;
 }
 
-hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root) {
+hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root, void *log) {
   utils::Assert(opened_, "peer group not opened");
   char *user = static_cast<char *>(buf);
+  char *lg = static_cast<char *>(log);
   for (size_t off = 0; off < bytes; off += stage_bytes_) {
     const size_t c = std::min(stage_bytes_, bytes - off);
     const int which = parity_;
     parity_ ^= 1;
-    if (rank_ == root) XRABIT_TRY_HIP(LaunchCopy(stage(root, which), user + off, c, stream_));
+    CopyBatch b;
+    if (rank_ == root) {
+      // the root's stage copy also fills its log slot (one read of the user buffer)
+      if (lg == nullptr) {
+        XRABIT_TRY_HIP(LaunchCopy(stage(root, which), user + off, c, stream_));
+      } else {
+        NewBatch(&b);
+        AddSeg(&b, stage(root, which), user + off, lg + off, c);
+        XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+      }
+    }
     XRABIT_TRY_HIP(Barrier());
     const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
     size_t lo, hi;
-    CopyBatch b;
-    NewBatch(&b);
     if (rank_ != root) {
       // scatter: pull my segment from the root (kept in my stage buffer for the others)
+      NewBatch(&b);
       SegRange(c, seg, rank_, &lo, &hi);
       AddSeg(&b, stage(rank_, which) + lo, stage(root, which) + lo, user + off + lo, hi - lo);
       XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     }
     XRABIT_TRY_HIP(Barrier());
     if (rank_ != root) {
+      // allgather of the segments; each one also lands in the log slot (dual store), and the
+      // own segment goes from the local stage into the log
       NewBatch(&b);
       for (int q = 0; q < n_; ++q) {
-        if (q == rank_) continue;
         SegRange(c, seg, q, &lo, &hi);
-        AddSeg(&b, user + off + lo, stage(q, which) + lo, nullptr, hi - lo);
+        if (q == rank_) {
+          if (lg != nullptr) AddSeg(&b, lg + off + lo, stage(rank_, which) + lo, nullptr, hi - lo);
+          continue;
+        }
+        AddSeg(&b, user + off + lo, stage(q, which) + lo, lg != nullptr ? lg + off + lo : nullptr,
+               hi - lo);
       }
       XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     }
@@ -558,9 +574,10 @@ hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root) {
 }
 
 hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
-                                 const std::vector<size_t> &size) {
+                                 const std::vector<size_t> &size, void *log) {
   utils::Assert(opened_, "peer group not opened");
   char *user = static_cast<char *>(buf);
+  char *lg = static_cast<char *>(log);
   for (size_t wlo = 0; wlo < total; wlo += stage_bytes_) {
     const size_t whi = std::min(total, wlo + stage_bytes_);
     const int which = parity_;
@@ -574,7 +591,9 @@ hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size
         const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
         if (z <= a) continue;
         if (p == rank_) {
-          AddSeg(&b, stage(rank_, which) + (a - wlo), user + a, nullptr, z - a);
+          // own slice into the stage (and the log slot, dual store)
+          AddSeg(&b, stage(rank_, which) + (a - wlo), user + a, lg != nullptr ? lg + a : nullptr,
+                 z - a);
         }
       }
     }
@@ -587,7 +606,10 @@ hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size
       const int k = SliceRanges(begin[p], size[p], total, lo, hi);
       for (int j = 0; j < k; ++j) {
         const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
-        if (z > a) AddSeg(&b, user + a, stage(p, which) + (a - wlo), nullptr, z - a);
+        if (z > a) {
+          AddSeg(&b, user + a, stage(p, which) + (a - wlo), lg != nullptr ? lg + a : nullptr,
+                 z - a);
+        }
       }
     }
     if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));

@@ -211,9 +211,11 @@ class PeerGroup {
   /*! \brief allreduce of count elements of type_nbytes bytes with a caller-provided reduction */
   hipError_t AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                              size_t type_nbytes, const ReduceStep &step);
-  hipError_t Broadcast(void *buf, size_t bytes, int root);
+  /*! \brief log != nullptr: every byte of the result is also stored there by the same
+   *  kernels (the robust engine's result-log slot: no copy after the collective) */
+  hipError_t Broadcast(void *buf, size_t bytes, int root, void *log = nullptr);
   hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
-                        const std::vector<size_t> &size);
+                        const std::vector<size_t> &size, void *log = nullptr);
   /*!
    * \brief point-to-point copies between ranks (a collective: every rank passes the same plan).
    *        Each sender streams the distinct payloads it owns through its stage buffer, one

@@ -113,6 +113,9 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
   if (is("rabit_rccl_tune")) rccl_tune_ = utils::StringToBool(val);
+  if (is("rabit_rccl_init_timeout_sec")) dcfg_.comm_init_timeout_sec = atof(val);
+  if (is("rabit_rccl_max_failures")) dcfg_.rccl_max_failures = atoi(val);
+  if (is("rabit_mock_rccl_error")) dcfg_.mock_rccl_error = atoi(val);
   if (is("rabit_rccl_tune_ctas")) rccl_tune_ctas_ = val;
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
@@ -435,7 +438,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   return dev_->Finish(MakeProbe());
 }
 
-Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
+Status EngineBase::TryBroadcast(void *buf, size_t size, int root, void *dev_log) {
   if (size == 0) return Status::kSuccess;
   if (!OnDevice(buf)) {
     if (GetWorldSize() == 1) return Status::kSuccess;
@@ -449,20 +452,27 @@ Status EngineBase::TryBroadcast(void *buf, size_t size, int root) {
     }
     return host_->TreeBroadcast(buf, size, root);
   }
-  if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   device::DeviceGuard dg(dev_->device());
+  if (GetWorldSize() == 1 && !world1_transport_) {
+    if (dev_log != nullptr) {
+      dev_->EnterFromUser();
+      dev_->CopyDeviceAsync(dev_log, buf, size);
+      return dev_->Finish(MakeProbe(), false);
+    }
+    return Status::kSuccess;
+  }
   Status s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
   dev_->EnterFromUser();
   MaybeInjectDeviceHang();
-  s = dev_->Broadcast(buf, size, root, MakeProbe());
+  s = dev_->Broadcast(buf, size, root, MakeProbe(), dev_log);
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
 }
 
 Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t end,
-                                size_t prev_size) {
+                                size_t prev_size, void *dev_log) {
   if (total == 0) return Status::kSuccess;
   if (!OnDevice(buf)) {
     if (GetWorldSize() == 1) return Status::kSuccess;
@@ -488,8 +498,15 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
     }
     return host_->RingAllgather(buf, total, begin, end, prev_size);
   }
-  if (GetWorldSize() == 1 && !world1_transport_) return Status::kSuccess;
   device::DeviceGuard dg(dev_->device());
+  if (GetWorldSize() == 1 && !world1_transport_) {
+    if (dev_log != nullptr) {
+      dev_->EnterFromUser();
+      dev_->CopyDeviceAsync(dev_log, buf, total);
+      return dev_->Finish(MakeProbe(), false);
+    }
+    return Status::kSuccess;
+  }
   // every rank needs every slice: exchange (begin, size) pairs over the host ring first
   const int n = GetWorldSize();
   std::vector<uint64_t> meta(2 * n, 0);
@@ -507,7 +524,7 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
   stats_.n_device_ops += 1;
   dev_->EnterFromUser();
   MaybeInjectDeviceHang();
-  s = dev_->AllgatherV(buf, total, b, z, MakeProbe());
+  s = dev_->AllgatherV(buf, total, b, z, MakeProbe(), dev_log);
   if (s != Status::kSuccess) return s;
   return dev_->Finish(MakeProbe());
 }
@@ -763,6 +780,10 @@ std::string EngineBase::StatsJson() const {
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"rccl_init_failed\":" << rccl_failed_
+     << ",\"rccl_calls\":" << (dev_ ? dev_->rccl_calls() : 0)
+     << ",\"rccl_settled\":" << (dev_ ? dev_->rccl_settled() : 0)
+     << ",\"rccl_aborts\":" << (dev_ ? dev_->rccl_aborts() : 0)
+     << ",\"rccl_init_abandoned\":" << (dev_ ? dev_->init_abandoned() : 0)
      << ",\"rccl_tuning\":" << rccl_tune_json_
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)

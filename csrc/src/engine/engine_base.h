@@ -162,8 +162,11 @@ class EngineBase : public IEngine {
    */
   Status TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec,
                             void *dst2 = nullptr, int prep = 0, double alpha = 1.0);
-  Status TryBroadcast(void *buf, size_t size, int root);
-  Status TryAllgather(void *buf, size_t total, size_t begin, size_t end, size_t prev_size);
+  /*! \brief dev_log (HBM buffers only): on success the result is also in dev_log, stored by
+   *  the transport itself (no copy after the collective on the direct path) */
+  Status TryBroadcast(void *buf, size_t size, int root, void *dev_log = nullptr);
+  Status TryAllgather(void *buf, size_t total, size_t begin, size_t end, size_t prev_size,
+                      void *dev_log = nullptr);
   /*! \brief build the device transports if missing (collective): exchange GPU records, map
    *  the peers' buffers for the direct transport, build the RCCL communicator */
   Status EnsureDeviceComm();

@@ -229,6 +229,11 @@ void EngineRobust::InitAfterException() {
 }
 
 // ------------------------------------------------------------------ helpers
+std::string EngineRobust::CallKey(const char *file, int line, const char *caller,
+                                  const std::string &shape) {
+  return std::string(file) + "::" + std::to_string(line) + "::" + caller + shape;
+}
+
 void EngineRobust::ApplyRetention() {
   const int last = resbuf_.LastSeqNo();
   if (last != -1 &&
@@ -333,9 +338,13 @@ void EngineRobust::AllreduceImpl(void *buf, const ReduceSpec &spec, PreprocFunct
     run_prepare();
     return;
   }
-  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
-                          "#" + std::to_string(spec.type_nbytes) + "x" +
-                          std::to_string(spec.count);
+  // the caller-signature key only serves the bootstrap cache and the debug log: built only
+  // when one of them is on (a string build per op is measurable on the small-op path)
+  const bool keyed = debug_ || (bootstrap_cache_ && !checkpoint_loaded_);
+  const std::string key =
+      keyed ? CallKey(_file, _line, _caller,
+                      "#" + std::to_string(spec.type_nbytes) + "x" + std::to_string(spec.count))
+            : std::string();
   if (!checkpoint_loaded_ && bootstrap_cache_ && GetBootstrapCache(key, buf, bytes) != -1) {
     return;
   }
@@ -401,8 +410,11 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
   if (GetWorldSize() == 1 && world1_fastpath_) return;
   if (total_size == 0) return;
   const bool dev = OnDevice(buf);
-  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
-                          "#" + std::to_string(total_size) + "@" + std::to_string(root);
+  const bool keyed = debug_ || (bootstrap_cache_ && !checkpoint_loaded_);
+  const std::string key =
+      keyed ? CallKey(_file, _line, _caller,
+                      "#" + std::to_string(total_size) + "@" + std::to_string(root))
+            : std::string();
   if (!checkpoint_loaded_ && bootstrap_cache_ &&
       GetBootstrapCache(key, buf, total_size) != -1) {
     return;
@@ -418,13 +430,12 @@ void EngineRobust::Broadcast(void *buf, size_t total_size, int root, const char 
       stats_.n_recovered_ops += 1;
       break;
     }
-    if (CheckAndRecover(TryBroadcast(buf, total_size, root))) {
+    // an HBM log slot is written by the collective itself (dual store), not copied after it
+    const bool log_in_op = dev && !resbuf_.temp_spilled();
+    if (CheckAndRecover(TryBroadcast(buf, total_size, root, log_in_op ? temp : nullptr))) {
       if (dev && resbuf_.temp_spilled()) {
         SpillResult(temp, buf, total_size);
-      } else if (dev) {
-        dev_->CopyDeviceAsync(temp, buf, total_size);
-        dev_->Finish(MakeProbe(), false);
-      } else {
+      } else if (!dev) {
         std::memcpy(temp, buf, total_size);
       }
       break;
@@ -457,8 +468,9 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
   if (GetWorldSize() == 1 && world1_fastpath_) return;
   if (total_size == 0) return;
   const bool dev = OnDevice(buf);
-  const std::string key = std::string(_file) + "::" + std::to_string(_line) + "::" + _caller +
-                          "#" + std::to_string(total_size);
+  const bool keyed = debug_ || (bootstrap_cache_ && !checkpoint_loaded_);
+  const std::string key =
+      keyed ? CallKey(_file, _line, _caller, "#" + std::to_string(total_size)) : std::string();
   if (!checkpoint_loaded_ && bootstrap_cache_ &&
       GetBootstrapCache(key, buf, total_size) != -1) {
     return;
@@ -476,13 +488,12 @@ void EngineRobust::Allgather(void *buf, size_t total_size, size_t slice_begin, s
     }
     // in place on the user buffer: the ring never overwrites this rank's own slice, so a
     // retry after a failure still finds its input
-    if (CheckAndRecover(TryAllgather(buf, total_size, slice_begin, slice_end, size_prev_slice))) {
+    const bool log_in_op = dev && !resbuf_.temp_spilled();
+    if (CheckAndRecover(TryAllgather(buf, total_size, slice_begin, slice_end, size_prev_slice,
+                                     log_in_op ? temp : nullptr))) {
       if (dev && resbuf_.temp_spilled()) {
         SpillResult(temp, buf, total_size);
-      } else if (dev) {
-        dev_->CopyDeviceAsync(temp, buf, total_size);
-        dev_->Finish(MakeProbe(), false);
-      } else {
+      } else if (!dev) {
         std::memcpy(temp, buf, total_size);
       }
       break;
@@ -519,6 +530,10 @@ void EngineRobust::LocalModelCheck(const Serializable *local_model) {
       local_.Configure(num_local_replica_ + 1, on_device, on_device ? dev_->device() : -1);
       local_.set_mirror_ctas(MirrorEngine() == device::DeviceCheckpoint::kEngineKernel
                                  ? std::max(mirror_ctas_, 1) : 0);
+      // the global checkpoint's mirror settings hold for the local state as well
+      local_.set_mirror_off(ckpt_mirror_mode_ == device::DeviceCheckpoint::kMirrorOff);
+      local_.set_mirror_sdma(on_device &&
+                             MirrorEngine() == device::DeviceCheckpoint::kEngineSdma);
     } else {
       use_local_model_ = 0;
       num_local_replica_ = 0;
@@ -659,6 +674,11 @@ void EngineRobust::CheckPointImpl(const Serializable *global_model,
     }
     RecoverExec(nullptr, 0, 0, ActionSummary::kLocalCheckAck, cur_cache_seq_, "CheckPoint");
     local_chkpt_version_ = nv;
+    // every rank passed kLocalCheckAck holding version nv: the superseded version can never be
+    // loaded again, so its slots are marked absent now.  A stale slot must not look present
+    // when the next checkpoint reuses this version (a holder picked by the recovery plan would
+    // serve a model from two checkpoints ago).
+    local_.Clear(!nv);
     if (local_.on_device()) local_.Mirror(nv, dev_->stream());
   }
   utils::Check(RecoverExec(nullptr, 0, ActionSummary::kCheckPoint, ActionSummary::kSpecialOp,
@@ -776,9 +796,13 @@ void EngineRobust::WatchdogLoop() {
     // a wait on this rank's own GPU that outlasts every deadline (a HIP call that blocks on a
     // wedged stream): nothing in this process can unblock it, so leave for a restart
     const double on_gpu = core::DeviceWaitingFor();
-    if (dev_wait_limit_sec_ > 0 && on_gpu > dev_wait_limit_sec_) {
-      fprintf(stderr, "[%d] xrabit: waiting on the GPU for %.1f s (rabit_device_wait_limit_sec=%g)\n",
-              wd_rank_.load(), on_gpu, dev_wait_limit_sec_);
+    const double gpu_limit = core::EffectiveDeviceWaitLimit(
+        dev_wait_limit_sec_, core::GlobalWaitState().device_op_deadline.load(),
+        dcfg_.drain_timeout_sec);
+    if (gpu_limit > 0 && on_gpu > gpu_limit) {
+      fprintf(stderr, "[%d] xrabit: waiting on the GPU for %.1f s (limit %.1f s: "
+              "rabit_device_wait_limit_sec=%g, op deadline %.1f s)\n", wd_rank_.load(), on_gpu,
+              gpu_limit, dev_wait_limit_sec_, core::GlobalWaitState().device_op_deadline.load());
       device::DevicePlane::WedgedExit("watchdog");
     }
     const double since = recovering_since_.load();

@@ -190,6 +190,9 @@ class EngineRobust : public EngineBase {
   void CheckPointImpl(const Serializable *global_model, const Serializable *local_model,
                       bool lazy);
   /*! \brief drop the previous result unless this rank is one of its replicas */
+  /*! \brief bootstrap-cache key of a call site (reference: `file::line::caller#shape`) */
+  static std::string CallKey(const char *file, int line, const char *caller,
+                             const std::string &shape);
   void ApplyRetention();
   /*! \brief copy an HBM result into its pinned spill slot (stream-ordered) */
   void SpillResult(void *slot, const void *src, size_t n);

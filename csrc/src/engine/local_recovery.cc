@@ -123,7 +123,7 @@ Status EngineRobust::TryCheckinLocalState(int v) {
     if (s == Status::kSuccess) {
       size_t got = 0;
       dev_->EnterFromUser();
-      s = dev_->Exchange(plan, &got);
+      s = dev_->Exchange(plan, &got, MakeProbe());
       if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
       if (s == Status::kSuccess) stats_.bytes_local_in += static_cast<double>(got);
     }
@@ -209,7 +209,7 @@ Status EngineRobust::TryRecoverLocalState(int v) {
     if (s == Status::kSuccess) {
       size_t got = 0;
       dev_->EnterFromUser();
-      s = dev_->Exchange(xs, &got);
+      s = dev_->Exchange(xs, &got, MakeProbe());
       if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
       if (s == Status::kSuccess) stats_.bytes_local_in += static_cast<double>(got);
     }

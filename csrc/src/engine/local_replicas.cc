@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "device/device_plane.h"
+#include "device/dma_copier.h"
 #include "device/kernels.h"
 #include "rabit/internal/utils.h"
 
@@ -16,6 +17,10 @@ namespace engine {
 LocalReplicas::~LocalReplicas() {
   if (!on_device_) return;
   (void)hipSetDevice(device_);
+  if (dma_) {
+    (void)dma_->WaitAll();  // the copier reads slot 0 and writes pinned_
+    dma_.reset();
+  }
   if (side_ != nullptr) (void)hipStreamSynchronize(side_);
   for (auto &v : slots_) {
     for (auto &s : v) {
@@ -93,16 +98,36 @@ size_t LocalReplicas::Bytes(int v) const {
   return b;
 }
 
+void LocalReplicas::set_mirror_sdma(bool sdma) {
+  dma_.reset();
+  if (!sdma || !on_device_) return;
+  std::unique_ptr<device::DmaCopier> d(new device::DmaCopier(device_));
+  if (d->ok()) {
+    dma_ = std::move(d);
+  } else {
+    utils::HandleLogInfo("[xrabit] SDMA local mirror unavailable (%s): using hipMemcpyAsync\n",
+                         d->why().c_str());
+  }
+}
+
 void LocalReplicas::Mirror(int v, hipStream_t stream) {
-  if (!on_device_ || !valid(v, 0) || slots_[v][0].size == 0) return;
+  if (!on_device_ || mirror_off_ || !valid(v, 0) || slots_[v][0].size == 0) return;
   device::DeviceGuard dg(device_);
   if (mirror_pending_) {
-    const hipError_t e = hipEventQuery(done_);
-    if (e == hipErrorNotReady) {
-      ++mirrors_skipped_;
-      return;
+    if (dma_) {
+      if (!dma_->Done(dma_ticket_)) {
+        ++mirrors_skipped_;
+        return;
+      }
+      (void)dma_->Wait(dma_ticket_);  // a failed mirror is simply superseded by this one
+    } else {
+      const hipError_t e = hipEventQuery(done_);
+      if (e == hipErrorNotReady) {
+        ++mirrors_skipped_;
+        return;
+      }
+      device::CheckHip(e, "local mirror");
     }
-    device::CheckHip(e, "local mirror");
     mirror_pending_ = false;
   }
   const size_t bytes = static_cast<size_t>(slots_[v][0].size);
@@ -113,6 +138,14 @@ void LocalReplicas::Mirror(int v, hipStream_t stream) {
     pinned_cap_ = bytes;
   }
   device::CheckHip(hipEventRecord(ready_, stream), "hipEventRecord");
+  if (dma_) {
+    // the copier's thread waits for ready_ and runs the copy on an SDMA engine (no CU time)
+    dma_ticket_ = dma_->Submit(pinned_, slots_[v][0].dev, bytes, ready_);
+    mirror_pending_ = true;
+    mirror_version_ = v;
+    ++mirrors_;
+    return;
+  }
   device::CheckHip(hipStreamWaitEvent(side_, ready_, 0), "hipStreamWaitEvent");
   device::CheckHip(mirror_ctas_ > 0
                        ? device::LaunchCopyNarrow(pinned_, slots_[v][0].dev, bytes, mirror_ctas_,
@@ -128,6 +161,12 @@ void LocalReplicas::Mirror(int v, hipStream_t stream) {
 void LocalReplicas::BeforeWrite(int v, hipStream_t stream) {
   if (!on_device_ || !mirror_pending_ || mirror_version_ != v) return;
   device::DeviceGuard dg(device_);
+  if (dma_) {
+    // an SDMA job is not on any stream: the host waits until it has read the slot
+    (void)dma_->Wait(dma_ticket_);
+    mirror_pending_ = false;
+    return;
+  }
   device::CheckHip(hipStreamWaitEvent(stream, done_, 0), "hipStreamWaitEvent(mirror)");
 }
 }  // namespace engine

@@ -21,10 +21,14 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 namespace rabit {
+namespace device {
+class DmaCopier;
+}
 namespace engine {
 
 class LocalReplicas {
@@ -76,6 +80,11 @@ class LocalReplicas {
   uint64_t mirrors_skipped() const { return mirrors_skipped_; }
   /*! \brief workgroups of the narrow D2H copy kernel of the mirror; 0: hipMemcpyAsync */
   void set_mirror_ctas(int c) { mirror_ctas_ = c; }
+  /*! \brief the checkpoint mirror settings of the engine (rabit_device_ckpt_mirror,
+   *  rabit_device_mirror_engine) apply to the local state too: off = no host mirror; sdma = the
+   *  copy runs on an SDMA engine (device/dma_copier.h) instead of a blit kernel */
+  void set_mirror_off(bool off) { mirror_off_ = off; }
+  void set_mirror_sdma(bool sdma);
 
  private:
   struct Slot {
@@ -98,6 +107,9 @@ class LocalReplicas {
   size_t pinned_cap_{0};
   bool mirror_pending_{false};
   int mirror_ctas_{0};
+  bool mirror_off_{false};
+  std::unique_ptr<device::DmaCopier> dma_;  // SDMA mirror engine (nullptr: HIP stream copy)
+  uint64_t dma_ticket_{0};
   int mirror_version_{-1};
   uint64_t mirrors_{0}, mirrors_skipped_{0};
 };

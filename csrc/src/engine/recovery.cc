@@ -380,7 +380,7 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
       if (s != Status::kSuccess) return s;
       size_t got = 0;
       dev_->EnterFromUser();
-      s = dev_->Exchange(plan, &got);
+      s = dev_->Exchange(plan, &got, MakeProbe());
       if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
       if (s == Status::kSuccess) {
         stats_.bytes_replay_in += static_cast<double>(got);
@@ -524,7 +524,7 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
   if (s != Status::kSuccess) return s;
   size_t got = 0;
   dev_->EnterFromUser();
-  s = dev_->Exchange(plan, &got);
+  s = dev_->Exchange(plan, &got, MakeProbe());
   if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
   if (s != Status::kSuccess) return s;
   stats_.bytes_ckpt_in += static_cast<double>(got);

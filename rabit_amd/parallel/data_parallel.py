@@ -97,7 +97,11 @@ class GradientBuckets:
         graphable=True: HBM buckets go through `rabit.allreduce_graphable` (a bare in-place
         ncclAllReduce on the current stream, no host synchronisation), so the call can sit
         inside a captured hipGraph with the rest of the step.  Non-fault-tolerant engines only
-        (init(lib="base")); averaging is one `mul_` on the same stream, captured as well."""
+        (init(lib="base")); averaging is one `mul_` on the same stream, captured as well.
+        Limits: a replayed graph has no deadline and no failure probe (a dead peer hangs
+        replay(); this is the base engine's contract), and multi-rank capture has only run with
+        a one-rank communicator so far (tests/scripts/graph_allreduce.py checks the reduced
+        values against world x the local gradient, so the first multi-GPU run verifies it)."""
         world = rabit.get_world_size()
         if graphable:
             for b in self.buckets:

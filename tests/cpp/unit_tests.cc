@@ -18,6 +18,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -29,6 +30,8 @@
 #include "engine/engine_mock.h"
 #include "engine/engine_robust.h"
 #include "engine/routing.h"
+#include "device/device_plane.h"
+#include "device/p2p_plan.h"
 
 namespace {
 struct TestCase {
@@ -447,6 +450,236 @@ void LoopbackPair(rabit::net::TcpSocket *a, rabit::net::TcpSocket *b) {
   EXPECT(a->Connect("127.0.0.1", port));
   *b = lis.Accept();
 }
+TEST(watchdog_device_wait_limit_clamp) {
+  using rabit::core::EffectiveDeviceWaitLimit;
+  EXPECT(EffectiveDeviceWaitLimit(0, 100, 30) == 0);       // watchdog off
+  EXPECT(EffectiveDeviceWaitLimit(600, 0, 30) == 600);     // no op deadline: the plain limit
+  EXPECT(EffectiveDeviceWaitLimit(600, 60, 30) == 600);    // op deadline well inside the limit
+  // an op deadline past the limit (explicit rabit_device_op_timeout, or the auto deadline of a
+  // very large op): the rank reaches its own deadline and drains before the watchdog fires
+  EXPECT(EffectiveDeviceWaitLimit(600, 900, 30) == 935);
+  EXPECT(EffectiveDeviceWaitLimit(600, rabit::device::AutoOpDeadline(size_t(700) << 30), 30) >
+         rabit::device::AutoOpDeadline(size_t(700) << 30) + 30);
+  {
+    rabit::core::DeviceDeadlineScope d(123);
+    EXPECT(rabit::core::GlobalWaitState().device_op_deadline.load() == 123);
+  }
+  EXPECT(rabit::core::GlobalWaitState().device_op_deadline.load() == 0);
+}
+
+// ---------------------------------------------------------------- RCCL p2p plans (offline)
+// The grouped ncclSend / ncclRecv paths of the device plane only run with two or more GPUs;
+// a send whose receive has a different size or order is a hang on the first real run.  These
+// tests check the plans device_plane.cc executes, for every rank of n = 2..8.
+namespace p2p = rabit::device;
+
+// every send s->d has a receive d<-s of equal bytes, in the same per-pair order
+void ExpectPaired(const std::vector<std::vector<p2p::P2POp>> &per_rank) {
+  const int n = static_cast<int>(per_rank.size());
+  for (int s = 0; s < n; ++s) {
+    for (int d = 0; d < n; ++d) {
+      if (s == d) continue;
+      std::vector<size_t> sends, recvs;
+      for (const auto &o : per_rank[s]) {
+        if (o.send && o.peer == d) sends.push_back(o.bytes);
+      }
+      for (const auto &o : per_rank[d]) {
+        if (!o.send && o.peer == s) recvs.push_back(o.bytes);
+      }
+      EXPECT(sends == recvs);
+    }
+    for (const auto &o : per_rank[s]) EXPECT(o.peer != s && o.peer >= 0 && o.peer < n);
+  }
+}
+
+TEST(p2p_segment_plan_pairs_and_covers) {
+  const size_t counts[] = {0, 1, 7, 255, 256, 257, 1000, 4097, 65536 + 3, 300000 + 17};
+  const size_t tns[] = {1, 2, 4, 8, 12};
+  for (int n = 2; n <= 8; ++n) {
+    for (size_t count : counts) {
+      for (size_t tn : tns) {
+        const p2p::SegmentPlan plan(count, tn, n);
+        // segments tile [0, count) exactly once, in rank order, starts 256-element aligned
+        size_t next = 0;
+        for (int k = 0; k < n; ++k) {
+          EXPECT(plan.lo(k) == next || plan.elems(k) == 0);
+          EXPECT(plan.lo(k) % 256 == 0 || plan.lo(k) == count);
+          next = std::max(next, plan.hi(k));
+        }
+        EXPECT(next == count);
+        std::vector<std::vector<p2p::P2POp>> scatter(n), gather(n);
+        for (int r = 0; r < n; ++r) {
+          scatter[r] = plan.ScatterOps(r);
+          gather[r] = plan.GatherOps(r);
+        }
+        ExpectPaired(scatter);
+        ExpectPaired(gather);
+        for (int r = 0; r < n; ++r) {
+          // scatter: rank r sends segment k (bytes of its input at lo(k)) to rank k, and receives
+          // its own segment from every other rank into inbox slot `sender`, inside the inbox
+          for (const auto &o : scatter[r]) {
+            if (o.send) {
+              EXPECT(o.buf == p2p::kBufIn && o.offset == plan.lo(o.peer) * tn &&
+                     o.bytes == plan.elems(o.peer) * tn);
+            } else {
+              EXPECT(o.buf == p2p::kBufInbox && o.offset == o.peer * plan.slot_bytes(r) &&
+                     o.bytes == plan.elems(r) * tn);
+              EXPECT(o.offset + o.bytes <= plan.inbox_bytes(r));
+              EXPECT(o.offset % 256 == 0);
+            }
+          }
+          // gather: every byte of the output lands once, at the segment's own offset
+          std::vector<int> covered(count * tn, 0);
+          for (size_t i = plan.lo(r) * tn; i < plan.hi(r) * tn; ++i) covered[i] += 1;
+          for (const auto &o : gather[r]) {
+            EXPECT(o.buf == p2p::kBufOut);
+            if (o.send) {
+              EXPECT(o.offset == plan.lo(r) * tn && o.bytes == plan.elems(r) * tn);
+            } else {
+              EXPECT(o.offset == plan.lo(o.peer) * tn && o.bytes == plan.elems(o.peer) * tn);
+              for (size_t i = o.offset; i < o.offset + o.bytes; ++i) covered[i] += 1;
+            }
+          }
+          bool once = true;
+          for (int c : covered) once = once && c == 1;
+          EXPECT(once);
+          // reduce passes: every rank's copy of segment r is reduced exactly once, the running
+          // result leads every pass after the first, at most 8 sources per pass
+          std::vector<int> used(n, 0);
+          const auto passes = plan.ReducePasses(r, 8);
+          EXPECT(passes.empty() == (plan.elems(r) == 0));
+          for (size_t p = 0; p < passes.size(); ++p) {
+            EXPECT(passes[p].size() <= 8 && !passes[p].empty());
+            EXPECT((passes[p][0] == -1) == (p > 0));
+            for (int k : passes[p]) {
+              if (k >= 0) used[k] += 1;
+            }
+          }
+          if (!passes.empty()) {
+            for (int k = 0; k < n; ++k) EXPECT(used[k] == 1);
+          }
+        }
+      }
+    }
+  }
+}
+
+TEST(p2p_reduce_passes_many_sources) {
+  // more ranks than sources per pass (the same plan with a small pass width)
+  const p2p::SegmentPlan plan(1 << 20, 4, 8);
+  const auto passes = plan.ReducePasses(3, 3);
+  std::vector<int> order;
+  for (const auto &p : passes) {
+    for (int k : p) {
+      if (k >= 0) order.push_back(k);
+    }
+  }
+  EXPECT(order == std::vector<int>({0, 1, 2, 3, 4, 5, 6, 7}));  // rank order: deterministic sums
+  EXPECT(passes.size() == 4);  // 3 + (acc + 2) + (acc + 2) + (acc + 1)
+}
+
+TEST(p2p_allgather_pieces_cover_slices) {
+  std::mt19937 rng(7);
+  for (int n = 2; n <= 8; ++n) {
+    for (int trial = 0; trial < 200; ++trial) {
+      // rabit's ring layout: slices back to back from a random start, wrapping past the end
+      const size_t total = 1 + rng() % 5000;
+      std::vector<size_t> begin(n), size(n);
+      size_t cut = rng() % total, left = total;
+      for (int r = 0; r < n; ++r) {
+        size[r] = r + 1 == n ? left : (left == 0 ? 0 : rng() % (left + 1));
+        left -= size[r];
+        begin[r] = cut;
+        cut = (cut + size[r]) % total;
+      }
+      std::vector<int> owner(total, -1), hits(total, 0);
+      for (const auto &p : p2p::AllgatherPieces(total, begin, size)) {
+        EXPECT(p.bytes > 0 && p.offset + p.bytes <= total);
+        for (size_t i = p.offset; i < p.offset + p.bytes; ++i) {
+          hits[i] += 1;
+          owner[i] = p.root;
+        }
+      }
+      // every byte comes exactly once, from the rank whose slice holds it
+      for (int r = 0; r < n; ++r) {
+        for (size_t j = 0; j < size[r]; ++j) EXPECT(owner[(begin[r] + j) % total] == r);
+      }
+      bool once = true;
+      for (int h : hits) once = once && h == 1;
+      EXPECT(once);
+    }
+  }
+  const std::vector<size_t> ub = {0, 10, 20}, us = {10, 10, 10};
+  EXPECT(p2p::AllgatherUniform(30, ub, us));
+  EXPECT(!p2p::AllgatherUniform(31, ub, us));
+  const std::vector<size_t> wb = {5, 15, 25};
+  EXPECT(!p2p::AllgatherUniform(30, wb, us));
+}
+
+TEST(p2p_exchange_ops_pair_in_order) {
+  struct Item {
+    int src, dst, key;
+    size_t bytes;
+  };
+  std::mt19937 rng(11);
+  for (int n = 2; n <= 8; ++n) {
+    for (int trial = 0; trial < 100; ++trial) {
+      std::vector<Item> plan;
+      const int m = 1 + rng() % 24;
+      for (int i = 0; i < m; ++i) {
+        plan.push_back({static_cast<int>(rng() % n), static_cast<int>(rng() % n), i,
+                        (rng() % 4 == 0) ? 0 : 1 + rng() % 100000});
+      }
+      std::vector<std::vector<p2p::P2POp>> per(n);
+      std::vector<std::vector<size_t>> item_of(n);
+      size_t locals = 0;
+      for (int r = 0; r < n; ++r) {
+        std::vector<size_t> local;
+        per[r] = p2p::ExchangeOps(plan, r, &item_of[r], &local);
+        EXPECT(item_of[r].size() == per[r].size());
+        for (size_t i : local) EXPECT(plan[i].src == r && plan[i].dst == r && plan[i].bytes > 0);
+        locals += local.size();
+      }
+      ExpectPaired(per);
+      // the k-th send s->d and the k-th receive d<-s serve the same plan item
+      for (int s = 0; s < n; ++s) {
+        for (int d = 0; d < n; ++d) {
+          if (s == d) continue;
+          std::vector<size_t> si, ri;
+          for (size_t i = 0; i < per[s].size(); ++i) {
+            if (per[s][i].send && per[s][i].peer == d) si.push_back(item_of[s][i]);
+          }
+          for (size_t i = 0; i < per[d].size(); ++i) {
+            if (!per[d][i].send && per[d][i].peer == s) ri.push_back(item_of[d][i]);
+          }
+          EXPECT(si == ri);
+        }
+      }
+      size_t want_local = 0, moved = 0;
+      for (const Item &x : plan) {
+        if (x.bytes != 0 && x.src == x.dst) want_local += 1;
+        if (x.bytes != 0 && x.src != x.dst) moved += 1;
+      }
+      size_t sends = 0;
+      for (int r = 0; r < n; ++r) {
+        for (const auto &o : per[r]) sends += o.send ? 1 : 0;
+      }
+      EXPECT(locals == want_local && sends == moved);
+    }
+  }
+}
+
+TEST(rccl_result_classes) {
+  using rabit::device::ClassifyRccl;
+  using rabit::device::RcclOutcome;
+  EXPECT(ClassifyRccl(0) == RcclOutcome::kOk);
+  EXPECT(ClassifyRccl(7) == RcclOutcome::kPending);
+  // what a dead or aborted peer produces: recoverable
+  for (int r : {1, 2, 3, 6}) EXPECT(ClassifyRccl(r) == RcclOutcome::kPeerFailure);
+  // usage errors of this library: fatal
+  for (int r : {4, 5, 8, 42}) EXPECT(ClassifyRccl(r) == RcclOutcome::kFatal);
+}
+
 }  // namespace
 
 TEST(link_reset_discards_stale_bytes) {

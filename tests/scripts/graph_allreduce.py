@@ -65,8 +65,12 @@ from rabit_amd.parallel import GradientBuckets  # noqa: E402
 torch.manual_seed(0)
 model = torch.nn.Sequential(torch.nn.Linear(64, 64, bias=False), torch.nn.Tanh(),
                             torch.nn.Linear(64, 8, bias=False)).to(dev)
-buckets = GradientBuckets(model.parameters(), bucket_mb=1.0)
+# no averaging: the replayed buckets must hold world x the local gradient (every rank computes
+# the same one from the same seed), which checks the reduction itself on a multi-GPU run; at
+# world 1 RCCL records a copy and this is the identity
+buckets = GradientBuckets(model.parameters(), bucket_mb=1.0, average=False)
 xs = torch.randn(32, 64, device=dev)
+local = torch.autograd.grad(model(xs).square().mean(), list(model.parameters()))
 
 
 def dp_step():
@@ -89,6 +93,9 @@ for b in buckets.buckets:
 g2.replay()
 torch.cuda.synchronize()
 assert all(torch.equal(a, b) for a, b in zip(eager, buckets.buckets)), "graphed DP step"
+world = rabit.get_world_size()
+for p, g in zip(model.parameters(), local):
+    assert torch.allclose(p.grad, g * world, rtol=1e-5, atol=1e-7), "replayed bucket != world x grad"
 assert rabit.stats()["device_rccl"] == 1, "no RCCL communicator: nothing was captured"
 print("GRAPHAR OK", flush=True)
 rabit.finalize()

@@ -44,3 +44,56 @@ def test_headline_printed_once_and_only_on_rank0():
              "bench.HEADLINE.update(rec={'metric': 'm'}, t=time.time(), rank=1)\ntime.sleep(30)")
     assert p.returncode == 0
     assert p.stdout.strip() == ""
+
+
+def test_headline_value_is_busbw_above_one_rank():
+    """BASELINE.json's metric is the allreduce bus bandwidth: `value` is busbw at N > 1 (the
+    whole-job aggregate is a separate field); at N = 1 busbw is 0 by definition and `value` is
+    the algbw, labelled as such"""
+    import importlib
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    size = 128 << 20
+    for n in (2, 4, 8):
+        bw = bench.bandwidths(n, size, 1e-3)
+        assert bw["value"] == bw["busbw_GBps"] and bw["value_is"] == "busbw_GBps"
+        assert abs(bw["busbw_GBps"] - bw["algbw_GBps"] * 2 * (n - 1) / n) < 0.02
+        assert abs(bw["aggregate_GBps"] - n * bw["algbw_GBps"]) < 0.05 * n
+    one = bench.bandwidths(1, size, 1e-3)
+    assert one["busbw_GBps"] == 0.0 and one["value"] == one["algbw_GBps"]
+    assert one["value_is"].startswith("algbw")
+
+
+def test_bench_torchrun_busbw_and_config5():
+    """GPU: bench.py under torch.distributed.run with 2 ranks sharing the box's GPU (the direct
+    transport carries the data): the headline `value` is the busbw, and the extras carry
+    BASELINE config 5 (256 MiB sum + checkpoint every iteration, and its overhead)"""
+    import pytest
+    pytest.importorskip("torch")
+    import socket
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                          "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--steps", "3", "--warmup", "1", "--variants", "0"],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["collective"] is True
+    assert rec["value"] == rec["busbw_GBps"] > 0 and rec["value_is"] == "busbw_GBps", rec
+    assert rec["sum_tdiff_speed_MiBps"] > 0 and rec["aggregate_GBps"] > rec["value"]
+    assert "post_headline_failure" not in rec, rec["post_headline_failure"]
+    ex = rec["extras"]
+    assert ex["config5_iter_us"] > 0 and ex["config5_sum_only_iter_us"] > 0, ex
+    assert "config5_ckpt_overhead_us" in ex, ex
+
+
+test_bench_torchrun_busbw_and_config5.pytestmark = [__import__("pytest").mark.gpu]

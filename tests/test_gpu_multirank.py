@@ -142,6 +142,7 @@ def test_bench_torchrun_shared_gpu(n):
     assert len(lines) == 1, out.stdout[-2000:]
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["value"] == rec["busbw_GBps"] and rec["value_is"] == "busbw_GBps", rec
     assert rec["transport"]["direct"] == 1, rec
     assert rec["result_check"], rec
     assert "post_headline_failure" not in rec, rec["post_headline_failure"]

@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from rabit_amd import ops  # noqa: E402
 
-HBM_ROOF_TBPS = 6.3  # measured float4 copy on MI355X (MI355X_MICROARCH.md)
+HBM_SPEC_TBPS = 8.0  # MI355X HBM3E spec; the achievable peak is measured in each run (below)
 
 
 def timeit(fn, reps, inner):
@@ -96,14 +96,22 @@ def main():
         for name, (fn, nbytes) in cases.items():
             med, best = timeit(fn, args.reps, args.inner)
             results[name].append((med, best, nbytes))
+    rows = []
     for name, vals in results.items():
         med = sorted(v[0] for v in vals)[len(vals) // 2]
         best = min(v[1] for v in vals)
         nbytes = vals[0][2]
+        rows.append((name, med, best, nbytes))
+    # the roof every percentage refers to: the best median bandwidth any streaming case (ours or
+    # torch's) reached in this run, so no figure can exceed 100 %; the 8 TB/s spec alongside
+    peak = max(nb / med for _, med, _, nb in rows)
+    for name, med, best, nbytes in rows:
         rec = {"kernel": name, "mib_per_operand": args.mb, "inner": args.inner,
                "median_us": round(med * 1e6, 1),
                "best_us": round(best * 1e6, 1), "GBps": round(nbytes / med / 1e9, 1),
-               "pct_hbm_roof": round(100 * nbytes / med / 1e12 / HBM_ROOF_TBPS, 1)}
+               "pct_of_measured_peak": round(100 * nbytes / med / peak, 1),
+               "measured_peak_GBps": round(peak / 1e9, 1),
+               "pct_of_hbm_spec": round(100 * nbytes / med / 1e12 / HBM_SPEC_TBPS, 1)}
         print(json.dumps(rec), flush=True)
 
 
