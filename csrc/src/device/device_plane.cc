@@ -223,21 +223,7 @@ DevicePlane::~DevicePlane() {
   (void)hipDeviceSynchronize();
   peers_.reset();
   if (comm_ != nullptr) {
-    // flush and release it; a non-blocking communicator finalizes asynchronously (bounded
-    // wait: a peer that is gone must not hold this process at exit)
-    ncclResult_t r = ncclCommFinalize(comm_);
-    ncclResult_t st = r;
-    const auto t0 = std::chrono::steady_clock::now();
-    while (r == ncclInProgress && ncclCommGetAsyncError(comm_, &st) == ncclSuccess &&
-           st == ncclInProgress &&
-           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10)) {
-      std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
-    if ((r == ncclSuccess || r == ncclInProgress) && st == ncclSuccess) {
-      ncclCommDestroy(comm_);
-    } else {
-      ncclCommAbort(comm_);
-    }
+    ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
   for (int i = 0; i < kScratchSlots; ++i) {
@@ -659,6 +645,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_fused_grid(cfg_.fused_grid);
     peers_->set_fused_oneshot_max(cfg_.fused_oneshot_max);
     peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
+    peers_->set_done_signal(cfg_.done_word);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();
@@ -714,6 +701,20 @@ void DevicePlane::EnterFromUser() {
 }
 
 Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
+  return WaitUntil([ev]() { return hipEventQuery(ev); }, probe);
+}
+
+Status DevicePlane::WaitWord(const volatile unsigned long long *word, unsigned long long epoch,
+                             const FailureProbe &probe) {
+  return WaitUntil(
+      [word, epoch]() {
+        return __atomic_load_n(word, __ATOMIC_ACQUIRE) >= epoch ? hipSuccess : hipErrorNotReady;
+      },
+      probe);
+}
+
+template <typename Poll>
+Status DevicePlane::WaitUntil(const Poll &poll, const FailureProbe &probe) {
   trace::Scope ts("device_wait", rank_, -1, -1, op_bytes_, 1);
   core::WaitScope waiting;  // peers' barriers and RCCL: waiting on other ranks
   core::DeviceWaitScope on_gpu;
@@ -722,7 +723,7 @@ Status DevicePlane::WaitEvent(hipEvent_t ev, const FailureProbe &probe) {
   const double limit = cfg_.op_timeout_sec < 0 ? AutoOpDeadline(op_bytes_) : cfg_.op_timeout_sec;
   core::DeviceDeadlineScope deadline(limit);  // the watchdog leaves this wait to the deadline
   for (uint64_t iter = 0;; ++iter) {
-    hipError_t e = hipEventQuery(ev);
+    hipError_t e = poll();
     if (e == hipSuccess) {
       if (peers_ != nullptr && peers_->failed()) {
         utils::HandleLogInfo("[xrabit] direct transport: a peer barrier gave up\n");
@@ -767,9 +768,19 @@ Status DevicePlane::Finish(const FailureProbe &probe, bool host_wait) {
   // release fence between back-to-back ops (tools/event_fence_probe.hip), and an op on the
   // caller's stream with no host wait needs none (stream order is the dependency)
   Status s = Status::kSuccess;
+  const volatile unsigned long long *word = nullptr;
+  unsigned long long epoch = 0;
+  const bool signalled = peers_ != nullptr && peers_->TakeDoneSignal(&word, &epoch);
   if (cfg_.sync && host_wait) {
-    CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
-    s = WaitEvent(ev_done_, probe);
+    if (signalled && pending_dst_ == nullptr) {
+      // the op's last kernel stores its completion into pinned host memory: poll that word
+      // (no event record / query round trips on the small-op path)
+      s = WaitWord(word, epoch, probe);
+      done_words_ += 1;
+    } else {
+      CheckHip(hipEventRecord(ev_done_, stream_), "hipEventRecord(done)");
+      s = WaitEvent(ev_done_, probe);
+    }
   }
   op_bytes_ = 0;
   if (s == Status::kSuccess) rccl_fail_streak_ = 0;

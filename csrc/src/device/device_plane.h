@@ -58,8 +58,10 @@ struct DeviceConfig {
   size_t sym_heap{0};                  // bytes of the symmetric (IPC-exported) heap, 0: none
   size_t oneshot_max{256u << 10};      // direct allreduce: one-shot up to this many bytes
   int direct_mode{0};                  // direct reduce-scatter: 0 calibrated, 1 pull, 2 push
-  int fused_mode{2};                   // direct two-shot chunks as one fused kernel: 0 never,
-                                       // 1 always, 2 as the calibration finds faster
+  int fused_mode{0};                   // direct two-shot chunks as one fused kernel: 0 never
+                                       // (default: the 5-launch form measured faster from
+                                       // 1 MiB up, profiles/r3_fused_vs_classic), 1 always,
+                                       // 2 as the calibration finds faster
   int fused_grid{0};                   // workgroups of a fused launch (0: automatic)
   size_t fused_oneshot_max{64u << 10}; // one-shot direct ops up to this size as one fused
                                        // launch (0: never; above it the 3-launch form)
@@ -71,6 +73,8 @@ struct DeviceConfig {
   // of every channel) runs on a helper thread watched by the failure probe and a deadline, so
   // a peer that dies mid-init costs kAborted / kTimeout instead of a hang (see InitComm)
   double comm_init_timeout_sec{120};   // deadline of communicator bring-up (0: none)
+  bool done_word{true};                // small direct ops: poll a kernel-written host word for
+                                       // completion instead of an event
   int rccl_max_failures{8};            // consecutive aborted RCCL ops before the error is fatal
   int mock_rccl_error{0};              // test hook: the n-th RCCL enqueue (1-based) fails with
                                        // ncclRemoteError instead of running
@@ -371,9 +375,18 @@ class DevicePlane {
   uint64_t rccl_aborts() const { return rccl_aborts_; }
   /*! \brief communicator bring-ups given up while RCCL's bootstrap still waited on a peer */
   uint64_t init_abandoned() const { return init_abandoned_; }
+  /*! \brief ops whose completion was read from a kernel-written host word */
+  uint64_t done_words() const { return done_words_; }
 
  private:
   Status WaitEvent(hipEvent_t ev, const FailureProbe &probe);
+  /*! \brief wait until a kernel stored `epoch` (or more) into the pinned host word */
+  Status WaitWord(const volatile unsigned long long *word, unsigned long long epoch,
+                  const FailureProbe &probe);
+  /*! \brief the completion wait: poll() returns hipSuccess / hipErrorNotReady / an error;
+   *  meanwhile RCCL async errors, the failure probe and the op deadline are watched */
+  template <typename Poll>
+  Status WaitUntil(const Poll &poll, const FailureProbe &probe);
   /*!
    * \brief map an RCCL return code to a Status: success; ncclInProgress (non-blocking
    *        communicator) is polled to completion under the probe and the op deadline; a result a
@@ -431,6 +444,7 @@ class DevicePlane {
   size_t op_bytes_{0};
   std::vector<PeerLinkInfo> links_;
   uint64_t rccl_calls_{0}, rccl_settled_{0}, rccl_aborts_{0}, init_abandoned_{0};
+  uint64_t done_words_{0};
   void *warm_{nullptr};  // 4 KiB of HBM for the bring-up's connection warm-up
   int rccl_fail_streak_{0};  // aborted RCCL ops since the last op that completed
 };

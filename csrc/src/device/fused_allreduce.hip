@@ -438,11 +438,29 @@ __global__ __launch_bounds__(kBlock, 4) void FusedAllreduceKernel(FusedAllreduce
  *        peer does after its reads of this one: no second hand-off is needed.  The grid is at
  *        most a few dozen workgroups, so every one is resident.
  */
+/*! \brief completion signal of a launch (FusedAllreduceArgs::done_word): the workgroup that
+ *  counts itself in last re-arms the counter and stores the epoch into pinned host memory */
+__device__ __forceinline__ void SignalDone(const FusedAllreduceArgs &a) {
+  if (a.done_word == nullptr || threadIdx.x != 0) return;
+  // this workgroup's stores (the result, possibly a peer's stage) are complete before it counts
+  // in; the host then sees the word only after every workgroup did
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned old =
+      __hip_atomic_fetch_add(a.done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == gridDim.x - 1) {
+    __hip_atomic_store(a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.done_word, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void FusedOneshotKernel(FusedAllreduceArgs a) {
   __shared__ int s_bad;
   __shared__ const char *s_in[kMaxPeers];
-  if (GroupFailed(a)) return;
+  if (GroupFailed(a)) {
+    SignalDone(a);
+    return;
+  }
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   const int n = a.n, r = a.rank;
@@ -461,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void FusedOneshotKernel(FusedAllreduceArgs 
     CopyPrep<T, false>(mine + lo, src + lo, hi - lo, a.prep, alpha, vsrc);
     Publish(a, 1, [&](int) { return ReadyFlag(a, r, i); });
     if (!Await(a, &s_bad, n, [&](int p) { return p == r ? nullptr : ReadyFlag(a, p, i); })) {
-      return;
+      break;  // failure recorded; still count in below
     }
     if (threadIdx.x < static_cast<unsigned>(n)) {
       s_in[threadIdx.x] = a.stage[threadIdx.x] + lo * sizeof(T);
@@ -487,6 +505,7 @@ __global__ __launch_bounds__(kBlock) void FusedOneshotKernel(FusedAllreduceArgs 
     }
     __syncthreads();  // s_in is rewritten by the next tile
   }
+  SignalDone(a);
 }
 
 template <typename T>

@@ -262,6 +262,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   const bool timed = timing_ && count <= chunk;
   auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
   bool did_fused = false;
+  done_pending_ = false;
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
     const int which = parity_;
@@ -363,7 +364,16 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;
+      const bool signal = done_signal_ && count <= chunk;  // single-launch op
+      if (signal) {
+        fa.done_count = done_count();
+        fa.done_word = done_word();
+      }
       XRABIT_TRY_HIP(LaunchFusedOneshot(fa, std::min(fa.tiles, fused_grid_), stream_));
+      if (signal) {
+        done_pending_ = true;
+        done_epoch_ = fa.epoch;
+      }
       ++oneshot_ops_;
       ++fused_oneshots_;
       did_fused = true;
@@ -526,6 +536,7 @@ void PeerGroup::CollectTiming() {
 
 hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root, void *log) {
   utils::Assert(opened_, "peer group not opened");
+  done_pending_ = false;
   char *user = static_cast<char *>(buf);
   char *lg = static_cast<char *>(log);
   for (size_t off = 0; off < bytes; off += stage_bytes_) {
@@ -576,6 +587,7 @@ hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root, void *log) {
 hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                                  const std::vector<size_t> &size, void *log) {
   utils::Assert(opened_, "peer group not opened");
+  done_pending_ = false;
   char *user = static_cast<char *>(buf);
   char *lg = static_cast<char *>(log);
   for (size_t wlo = 0; wlo < total; wlo += stage_bytes_) {
@@ -618,6 +630,7 @@ hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size
 }
 hipError_t PeerGroup::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in) {
   utils::Assert(opened_, "peer group not opened");
+  done_pending_ = false;
   *bytes_in = 0;
   // every sender's distinct payloads, back to back (256-B aligned) in plan order: the byte
   // stream it pushes through its stage buffer.  All ranks derive the same layout.

@@ -127,6 +127,12 @@ struct FusedAllreduceArgs {
   const volatile int *abort_word;
   int *dev_status, *host_status;
   long long deadline_ticks;
+  // optional completion signal (fused one-shot): every workgroup counts itself in on done_count
+  // (device memory, re-armed by the last one), and the last one stores `epoch` into done_word
+  // (pinned host memory) — the host polls that word instead of an event (no hipEventRecord /
+  // hipEventQuery round trips on the small-op path)
+  unsigned int *done_count;
+  unsigned long long *done_word;
 };
 /*! \brief u64 words of one fused flag block (one parity) for tiles_cap tiles per segment */
 inline size_t FusedFlagWords(int tiles_cap) {
@@ -261,6 +267,20 @@ class PeerGroup {
   void set_fused_min_bytes(size_t b) { fused_min_bytes_ = b; }
   int fused_grid() const { return fused_grid_; }
   uint64_t fused_chunks() const { return fused_chunks_; }
+  /*!
+   * \brief the op just enqueued ends with a kernel that signals its completion in pinned host
+   *        memory: *word reaches `epoch` once every workgroup is done (failed ones included;
+   *        failed() tells).  False (and nothing to poll) otherwise.  Consumes the signal.
+   */
+  bool TakeDoneSignal(const volatile unsigned long long **word, unsigned long long *epoch) {
+    if (!done_pending_) return false;
+    done_pending_ = false;
+    *word = done_word();
+    *epoch = done_epoch_;
+    return true;
+  }
+  /*! \brief polling the done word instead of an event (rabit_device_done_word) */
+  void set_done_signal(bool v) { done_signal_ = v; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
   void EnableTiming();
   /*! \brief stop timing phases (the events stay for a later EnableTiming) */
@@ -296,6 +316,12 @@ class PeerGroup {
                                                   static_cast<size_t>(which) * fused_block_bytes_);
   }
   int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
+  unsigned int *done_count() const {
+    return reinterpret_cast<unsigned int *>(base_ + kPeerStatusOffset + 256);
+  }
+  unsigned long long *done_word() const {
+    return reinterpret_cast<unsigned long long *>(host_words_ + 8);  // bytes 32..39
+  }
   void NewBatch(CopyBatch *b) const {
     b->n = 0;
     b->guard = dev_status();
@@ -336,6 +362,9 @@ class PeerGroup {
   size_t fused_block_bytes_{0};     // bytes of one fused flag block (2 per allocation)
   unsigned long long fused_epoch_{0};
   uint64_t fused_chunks_{0};
+  bool done_signal_{true};
+  bool done_pending_{false};
+  unsigned long long done_epoch_{0};
 };
 
 }  // namespace device

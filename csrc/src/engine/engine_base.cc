@@ -116,6 +116,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_rccl_init_timeout_sec")) dcfg_.comm_init_timeout_sec = atof(val);
   if (is("rabit_rccl_max_failures")) dcfg_.rccl_max_failures = atoi(val);
   if (is("rabit_mock_rccl_error")) dcfg_.mock_rccl_error = atoi(val);
+  if (is("rabit_device_done_word")) dcfg_.done_word = utils::StringToBool(val);
   if (is("rabit_rccl_tune_ctas")) rccl_tune_ctas_ = val;
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {
@@ -784,6 +785,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"rccl_settled\":" << (dev_ ? dev_->rccl_settled() : 0)
      << ",\"rccl_aborts\":" << (dev_ ? dev_->rccl_aborts() : 0)
      << ",\"rccl_init_abandoned\":" << (dev_ ? dev_->init_abandoned() : 0)
+     << ",\"done_word_waits\":" << (dev_ ? dev_->done_words() : 0)
      << ",\"rccl_tuning\":" << rccl_tune_json_
      << ",\"direct_push\":" << (dev_ && dev_->direct_push() ? 1 : 0)
      << ",\"push_chunks\":" << (dev_ ? dev_->push_chunks() : 0)

@@ -60,7 +60,6 @@ def main():
                 rabit.allreduce(x, rabit.SUM)
             torch.cuda.synchronize()
             assert torch.equal(x, want), (form, nbytes)
-            rabit.set_phase_timing(not fused)
             before = rabit.stats()
             times = []
             for _ in range(args.reps):
@@ -70,7 +69,14 @@ def main():
                 torch.cuda.synchronize()
                 times.append(time.perf_counter() - t0)
             st = rabit.stats()
-            rabit.set_phase_timing(False)
+            if not fused:
+                # per-phase hipEvent times in a separate pass (the events cost time themselves)
+                rabit.set_phase_timing(True)
+                for _ in range(5):
+                    rabit.allreduce(x, rabit.SUM)
+                torch.cuda.synchronize()
+                st = dict(st, direct_phase_us=rabit.stats().get("direct_phase_us"))
+                rabit.set_phase_timing(False)
             times.sort()
             rec = {"form": form, "bytes": nbytes, "median_us": round(times[len(times) // 2] * 1e6, 1),
                    "min_us": round(times[0] * 1e6, 1), "reps": args.reps,
