@@ -33,10 +33,15 @@ assert below == 0 or thr >= 2 ** 63, (below, thr)
 assert st["calib_push_us"] > 0, st
 push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
 assert push in (0, world), push
-# all four forms of the two-shot path (pull/push x classic/fused) were timed and verified, and
-# the chosen form is the same everywhere
+# the forms of the two-shot path were timed and verified (pull/push x classic; the fused forms
+# too with rabit_device_fused=auto), and the chosen form is the same everywhere
 forms = st["calib_forms_us"]
-assert len(forms) == 4 and all(f > 0 for f in forms), forms
+fused_auto = "rabit_device_fused=auto" in sys.argv[1:]
+assert len(forms) == 4 and forms[0] > 0 and forms[2] > 0, forms
+if fused_auto:
+    assert all(f > 0 for f in forms), forms
+else:
+    assert forms[1] == -1 and forms[3] == -1 and st["direct_fused"] == 0, (forms, st)
 fused = rabit.allreduce(np.array([st["direct_fused"]]), rabit.SUM)[0]
 assert fused in (0, world), fused
 # with a symmetric heap that has room, the calibration reads its inputs from the heap's tail

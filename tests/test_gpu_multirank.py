@@ -91,7 +91,8 @@ def test_host_buffers_via_device():
     assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
 
 
-@pytest.mark.parametrize("extra", [[], ["rabit_device_symmetric_heap=160M"]])
+@pytest.mark.parametrize("extra", [[], ["rabit_device_symmetric_heap=160M"],
+                                   ["rabit_device_fused=auto"]])
 def test_calibration_flow(extra):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
