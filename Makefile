@@ -28,8 +28,11 @@ CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc 
              csrc/src/coll/host_coll.cc csrc/src/coll/shm_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc csrc/src/device/dma_copier.cc csrc/src/device/peer_coll.cc \
              csrc/src/engine/engine_base.cc csrc/src/engine/device_setup.cc csrc/src/engine/engine_robust.cc \
              csrc/src/engine/recovery.cc csrc/src/engine/local_replicas.cc csrc/src/engine/local_recovery.cc \
-             csrc/src/capi/c_api.cc
+             csrc/src/capi/c_api.cc csrc/src/capi/build_info.cc
 CORE_OBJS := $(patsubst csrc/src/%.cc,$(OBJ)/%.o,$(CORE_SRCS))
+# every source of the libraries, in byte order; their sha256 is compiled into build_info.o
+# (rabit_amd/_lib.py:source_hash computes the same over the working tree)
+ALL_SRCS  := $(shell find csrc -type f \( -name '*.cc' -o -name '*.h' -o -name '*.hip' \) | LC_ALL=C sort)
 KERN_OBJ  := $(OBJ)/device/kernels.o $(OBJ)/device/peer_kernels.o $(OBJ)/device/fused_allreduce.o
 HEADERS   := $(shell find csrc -name '*.h')
 
@@ -47,6 +50,11 @@ $(OBJ)/%.o: csrc/src/%.cc $(HEADERS)
 $(OBJ)/device/%.o: csrc/src/device/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/capi/build_info.o: csrc/src/capi/build_info.cc $(ALL_SRCS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -DXRABIT_ARCH='"$(ARCH)"' \
+	  -DXRABIT_SRC_HASH='"'"$$(cat $(ALL_SRCS) | sha256sum | cut -d' ' -f1)"'"' -c $< -o $@
 
 # one registry object per flavour: only the default engine differs
 $(OBJ)/registry_%.o: csrc/src/engine/registry.cc $(HEADERS)

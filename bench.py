@@ -214,6 +214,38 @@ def run_extras(rabit, torch, dev, world):
     out["broadcast_1GiB_ms"] = round(t * 1e3, 3)
     out["broadcast_1GiB_busbw_GBps"] = round(nb / t / 1e9, 2) if world > 1 else None
     out["broadcast_check"] = ok
+    if world > 1:
+        # the same broadcast on each transport that is up (the routed one above is the
+        # broadcast calibration's choice), each checked
+        st0 = rabit.stats()
+        per = {}
+        for name, which in (("rccl", rabit.TRANSPORT_RCCL), ("direct", rabit.TRANSPORT_DIRECT)):
+            phase("broadcast %s" % name)
+            up = rabit.set_device_transport(which, None)
+            if which == rabit.TRANSPORT_DIRECT and up:
+                up = rabit.set_device_transport(which, "push" if st0.get("direct_push") else "pull",
+                                                bool(st0.get("direct_fused")))
+            up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
+            if not up:
+                continue
+            blob.fill_(7 if rabit.get_rank() == 0 else 0)
+            rabit.broadcast_tensor(blob, 0)
+            good = bool((blob[:: 1 << 20] == 7).all().item())
+            tt = _timed(rabit, torch, lambda: rabit.broadcast_tensor(blob, 0), 3)
+            per[name] = {"ms": round(tt * 1e3, 3), "busbw_GBps": round(nb / tt / 1e9, 2),
+                         "check": good}
+            rabit.checkpoint(None)
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
+        if st0.get("device_direct"):
+            rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+                                       bool(st0.get("direct_fused")))
+        out["broadcast_1GiB_by_transport"] = per
+        st1 = rabit.stats()
+        out["broadcast_routing"] = {"calibration_us": dict(zip(
+            ["rccl_64KiB", "rccl_big", "direct_64KiB", "direct_big"], st1.get("calib_bcast_us", []))),
+            "direct_min_bytes": st1.get("bcast_direct_min"),
+            "direct_below_bytes": st1.get("bcast_direct_below"),
+            "direct_bcast_chunks": st1.get("direct_bcast_chunks")}
     del blob
     rabit.checkpoint(None)  # clears the result log (keeps HBM use bounded)
     # config 4: lazy allreduce, prepare = per-element squared gradient, 64 MiB

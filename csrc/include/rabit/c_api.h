@@ -57,6 +57,8 @@ RABIT_DLL int RabitLinkTag(void);
 // ---------------- xrabit extensions ----------------
 /*! \brief name of the active engine ("robust", "base", "mock", "empty") */
 RABIT_DLL const char *RabitEngineName(void);
+/*! \brief JSON: sha256 of the library's sources (csrc/), device code target, compile time */
+RABIT_DLL const char *RabitBuildInfo(void);
 /*! \brief order device collectives after the given hipStream_t (NULL = null stream) */
 RABIT_DLL void RabitSetStream(void *hip_stream);
 /*! \brief device ordinal of the engine, -1 if none */

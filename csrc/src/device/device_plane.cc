@@ -303,6 +303,16 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
     (void)hipSetDevice(dev);
     ncclComm_t c = nullptr;
     ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &config);
+    {
+      // given up on while the init blocked: the plane (its warm-up stream and buffer) may be
+      // gone already, so touch nothing of it
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (g->abandoned) {
+        g->done = true;
+        if (c != nullptr) ncclCommAbort(c);
+        return;
+      }
+    }
     if (r == ncclSuccess && nranks > 1) {
       // every p2p pair (RCCL connects send/recv channels lazily inside ncclGroupEnd) and the
       // allreduce path, with 1-byte / 1-element payloads
@@ -646,6 +656,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_fused_oneshot_max(cfg_.fused_oneshot_max);
     peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
     peers_->set_done_signal(cfg_.done_word);
+    peers_->set_bcast_chunk(cfg_.bcast_chunk);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();
@@ -990,7 +1001,7 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
 Status DevicePlane::Broadcast(void *buf, size_t bytes, int root, const FailureProbe &probe,
                               void *log) {
   op_bytes_ = bytes;
-  if (UseDirect(bytes)) {
+  if (UseDirectBcast(bytes)) {
     CheckHip(peers_->Broadcast(buf, bytes, root, log), "direct broadcast");
     return Status::kSuccess;
   }

@@ -67,6 +67,7 @@ struct DeviceConfig {
                                        // launch (0: never; above it the 3-launch form)
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
   size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
+  size_t bcast_chunk{0};               // direct broadcast pipeline chunk (0: sqrt(S x 4 MiB))
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
   int rccl_max_ctas{0};
   // RCCL communicator lifecycle: the bring-up (init and the connection
@@ -230,6 +231,24 @@ class DevicePlane {
     return comm_ == nullptr || cfg_.algo == 2 || bytes >= cfg_.direct_min_bytes ||
            bytes < direct_below_bytes_;
   }
+  /*! \brief route a broadcast of this many bytes over the direct transport: by its own
+   *  calibration once that ran (a broadcast moves each byte once per link, an allreduce twice,
+   *  so the crossover differs), by the allreduce routing before */
+  bool UseDirectBcast(size_t bytes) const {
+    if (peers_ == nullptr) return false;
+    if (force_ >= 0 || !bcast_routed_ || comm_ == nullptr || cfg_.algo == 2) return UseDirect(bytes);
+    return bytes >= bcast_min_bytes_ || bytes < bcast_below_bytes_;
+  }
+  void set_bcast_routing(size_t min_bytes, size_t below_bytes) {
+    bcast_routed_ = true;
+    bcast_min_bytes_ = min_bytes;
+    bcast_below_bytes_ = below_bytes;
+  }
+  bool bcast_routed() const { return bcast_routed_; }
+  size_t bcast_min_bytes() const { return bcast_min_bytes_; }
+  size_t bcast_below_bytes() const { return bcast_below_bytes_; }
+  uint64_t bcast_ops() const { return peers_ ? peers_->bcast_ops() : 0; }
+  uint64_t bcast_chunks() const { return peers_ ? peers_->bcast_chunks() : 0; }
   void set_direct_min_bytes(size_t b) { cfg_.direct_min_bytes = b; }
   /*! \brief ops below this size go direct too (the calibration found the direct transport
    *  faster for small ops and RCCL for large ones) */
@@ -431,6 +450,8 @@ class DevicePlane {
   size_t heap_used_{0};
   int force_{-1};
   size_t direct_below_bytes_{0};
+  bool bcast_routed_{false};
+  size_t bcast_min_bytes_{static_cast<size_t>(-1)}, bcast_below_bytes_{0};
   void *pending_dst_{nullptr};  // second destination of the last RCCL allreduce (see Finish)
   const void *pending_src_{nullptr};
   size_t pending_bytes_{0};

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "device/bcast_plan.h"
 #include "device/device_plane.h"
 #include "device/kernels.h"
 #include "rabit/internal/utils.h"
@@ -539,48 +540,39 @@ hipError_t PeerGroup::Broadcast(void *buf, size_t bytes, int root, void *log) {
   done_pending_ = false;
   char *user = static_cast<char *>(buf);
   char *lg = static_cast<char *>(log);
-  for (size_t off = 0; off < bytes; off += stage_bytes_) {
-    const size_t c = std::min(stage_bytes_, bytes - off);
-    const int which = parity_;
-    parity_ ^= 1;
-    CopyBatch b;
-    if (rank_ == root) {
-      // the root's stage copy also fills its log slot (one read of the user buffer)
-      if (lg == nullptr) {
-        XRABIT_TRY_HIP(LaunchCopy(stage(root, which), user + off, c, stream_));
-      } else {
-        NewBatch(&b);
-        AddSeg(&b, stage(root, which), user + off, lg + off, c);
-        XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
-      }
-    }
-    XRABIT_TRY_HIP(Barrier());
-    const size_t seg = RoundUp((c + n_ - 1) / n_, 256);
-    size_t lo, hi;
-    if (rank_ != root) {
-      // scatter: pull my segment from the root (kept in my stage buffer for the others)
-      NewBatch(&b);
-      SegRange(c, seg, rank_, &lo, &hi);
-      AddSeg(&b, stage(rank_, which) + lo, stage(root, which) + lo, user + off + lo, hi - lo);
-      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
-    }
-    XRABIT_TRY_HIP(Barrier());
-    if (rank_ != root) {
-      // allgather of the segments; each one also lands in the log slot (dual store), and the
-      // own segment goes from the local stage into the log
-      NewBatch(&b);
-      for (int q = 0; q < n_; ++q) {
-        SegRange(c, seg, q, &lo, &hi);
-        if (q == rank_) {
-          if (lg != nullptr) AddSeg(&b, lg + off + lo, stage(rank_, which) + lo, nullptr, hi - lo);
-          continue;
-        }
-        AddSeg(&b, user + off + lo, stage(q, which) + lo, lg != nullptr ? lg + off + lo : nullptr,
-               hi - lo);
-      }
-      XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
-    }
+  if (bytes == 0) return hipSuccess;
+  CopyBatch b;
+  if (n_ == 1) {
+    // a one-rank group: the data is already in place, only the log slot needs it
+    if (lg != nullptr) XRABIT_TRY_HIP(LaunchCopy(lg, user, bytes, stream_));
+    return hipSuccess;
   }
+  // scatter of chunk k+1 and allgather of chunk k in the same round (bcast_plan.h)
+  const size_t chunk = bcast_chunk_ != 0 ? std::min(bcast_chunk_, stage_bytes_)
+                                         : BcastPipeline::AutoChunk(bytes, stage_bytes_);
+  const BcastPipeline plan(bytes, chunk, n_, root);
+  const int base = parity_;
+  for (size_t t = 0; t < plan.rounds(); ++t) {
+    if (plan.barrier_before(t)) XRABIT_TRY_HIP(Barrier());
+    NewBatch(&b);
+    for (const BcastCopy &c : plan.Round(rank_, t)) {
+      const int which = BcastPipeline::parity(base, c.chunk);
+      const size_t at = c.chunk * plan.chunk + c.off;  // byte offset in the user buffer
+      const char *src = c.from < 0 ? user + at : stage(c.from, which) + c.off;
+      char *dsts[3];
+      int nd = 0;
+      if (c.to_stage) dsts[nd++] = stage(rank_, which) + c.off;
+      if (c.to_user) dsts[nd++] = user + at;
+      if (c.to_log && lg != nullptr) dsts[nd++] = lg + at;
+      utils::Assert(nd <= 2, "broadcast plan: more than two destinations");
+      if (nd == 0) continue;
+      AddSeg(&b, dsts[0], src, nd > 1 ? dsts[1] : nullptr, c.bytes);
+    }
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+  }
+  parity_ = plan.next_parity(base);
+  ++bcast_ops_;
+  bcast_chunks_ += plan.nchunks;
   return hipSuccess;
 }
 

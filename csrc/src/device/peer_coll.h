@@ -217,9 +217,18 @@ class PeerGroup {
   /*! \brief allreduce of count elements of type_nbytes bytes with a caller-provided reduction */
   hipError_t AllreduceCustom(const void *send, void *recv, void *recv2, size_t count,
                              size_t type_nbytes, const ReduceStep &step);
-  /*! \brief log != nullptr: every byte of the result is also stored there by the same
-   *  kernels (the robust engine's result-log slot: no copy after the collective) */
+  /*!
+   * \brief broadcast from root, pipelined over chunks: the scatter of chunk k+1 (root -> its
+   *        non-roots) and the allgather of chunk k (among the non-roots) share a round, because
+   *        they use disjoint xGMI link directions (bcast_plan.h).  log != nullptr: every byte of
+   *        the result is also stored there by the same kernels (the robust engine's result-log
+   *        slot: no copy after the collective)
+   */
   hipError_t Broadcast(void *buf, size_t bytes, int root, void *log = nullptr);
+  /*! \brief pipeline chunk of a broadcast (0: automatic, BcastPipeline::AutoChunk) */
+  void set_bcast_chunk(size_t b) { bcast_chunk_ = b; }
+  uint64_t bcast_ops() const { return bcast_ops_; }
+  uint64_t bcast_chunks() const { return bcast_chunks_; }
   hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                         const std::vector<size_t> &size, void *log = nullptr);
   /*!
@@ -363,6 +372,8 @@ class PeerGroup {
   unsigned long long fused_epoch_{0};
   uint64_t fused_chunks_{0};
   bool done_signal_{true};
+  size_t bcast_chunk_{0};
+  uint64_t bcast_ops_{0}, bcast_chunks_{0};
   bool done_pending_{false};
   unsigned long long done_epoch_{0};
 };

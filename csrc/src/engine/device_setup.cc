@@ -100,6 +100,10 @@ Status EngineBase::EnsureDeviceComm() {
       calibrate_) {
     s = CalibrateDevice();
     if (s != Status::kSuccess) return s;
+    if (dev_->has_peers()) {
+      s = CalibrateBroadcast();
+      if (s != Status::kSuccess) return s;
+    }
   }
   if (debug_) {
     utils::HandleLogInfo("[%d] device transport epoch %d: rccl=%d direct=%d (direct for >= %zu B)\n",
@@ -395,6 +399,108 @@ Status EngineBase::CalibrateDevice() {
                    : (dev_->direct_below_bytes() > 0
                           ? ("below " + std::to_string(dev_->direct_below_bytes()) + " B").c_str()
                           : "off (RCCL faster)")));
+  }
+  return Status::kSuccess;
+}
+
+Status EngineBase::CalibrateBroadcast() {
+  // byte sizes: a latency point and the allreduce calibration's large point (one stage)
+  const size_t big = std::min<size_t>(dcfg_.calib_big, dcfg_.peer_stage);
+  const size_t sizes[2] = {64u << 10, std::max<size_t>(big, 1u << 20) / 256 * 256};
+  char *buf = static_cast<char *>(dev_->Scratch(sizes[1], 1));
+  char *log = static_cast<char *>(dev_->Scratch(sizes[1], device::DevicePlane::kCalibScratch));
+  constexpr int kReps = 4;
+  const float want = 3.0f + (kReps - 1);  // root 0's value in the last repetition
+  double t[2][2] = {{0, 0}, {0, 0}};     // [transport: 0 rccl, 1 direct][size]
+  int ok = 1;
+  dev_->SetPeerDeadline(5.0);
+  // timed broadcast from root 0 into buf and the log slot (as the robust engine runs it: the
+  // direct kernels store both, RCCL copies into the log after the collective); every other
+  // rank's buffer holds -1 before each repetition, so stale bytes cannot pass the check
+  auto measure = [&](int which, int k, Status *st) {
+    const size_t count = sizes[k] / 4;
+    dev_->ForceTransport(which == 0 && !dev_->has_comm() ? 1 : which);
+    double best = 1e30;
+    for (int rep = 0; rep < kReps; ++rep) {
+      device::CheckHip(device::LaunchFill(buf, count, mpi::kFloat, rank_ == 0 ? 3.0 + rep : -1.0,
+                                          dev_->stream()),
+                       "LaunchFill");
+      *st = dev_->Finish(MakeProbe());
+      if (*st != Status::kSuccess) return false;
+      const double t0 = utils::GetTime();
+      *st = dev_->Broadcast(buf, sizes[k], 0, MakeProbe(), log);
+      if (*st == Status::kSuccess) *st = dev_->Finish(MakeProbe());
+      if (*st != Status::kSuccess) return false;
+      dev_->Synchronize();
+      if (rep > 0) best = std::min(best, utils::GetTime() - t0);
+    }
+    t[which][k] = best;
+    return true;
+  };
+  std::vector<float> host;
+  auto verified = [&](size_t bytes) {
+    for (char *p : {buf, log}) {
+      host.resize(bytes / 4);
+      dev_->StageToHost(host.data(), p, bytes);
+      for (float v : host) {
+        if (v != want) return false;
+      }
+    }
+    return true;
+  };
+  // 1. direct (a failed barrier leaves this phase within the 5 s deadline on every rank)
+  int correct = 1;
+  for (int k = 0; k < 2 && ok; ++k) {
+    Status st;
+    if (!measure(1, k, &st)) {
+      ok = 0;
+      break;
+    }
+    if (correct && !verified(sizes[k])) {
+      correct = 0;
+      utils::HandleLogInfo("[%d] direct broadcast verification failed (%zu B)\n", rank_, sizes[k]);
+    }
+  }
+  dev_->ForceTransport(-1);
+  dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
+  int flags[2] = {ok, correct};
+  Status s = host_->Allreduce(flags, sizeof(int), 2, coll::HostReducer(mpi::kInt, mpi::kMin));
+  if (s != Status::kSuccess) return s;
+  if (!flags[0]) {
+    // the group failed a barrier: no direct transport for anything (as CalibrateDevice does)
+    dev_->DropPeers();
+    return Status::kSuccess;
+  }
+  // 2. RCCL
+  for (int k = 0; k < 2; ++k) {
+    Status st;
+    if (!measure(0, k, &st)) {
+      dev_->ForceTransport(-1);
+      return st;  // RCCL failed: a real failure, the caller recovers
+    }
+  }
+  dev_->ForceTransport(-1);
+  double agg[4] = {t[0][0], t[0][1], t[1][0], t[1][1]};
+  s = host_->Allreduce(agg, sizeof(double), 4, coll::HostReducer(mpi::kDouble, mpi::kMax));
+  if (s != Status::kSuccess) return s;
+  for (int i = 0; i < 4; ++i) calib_bcast_[i] = agg[i];
+  if (!flags[1]) {
+    dev_->set_bcast_routing(static_cast<size_t>(-1), 0);  // a wrong direct result: RCCL only
+  } else {
+    const DirectRouting route = ChooseDirectRouting(static_cast<double>(sizes[0]),
+                                                    static_cast<double>(sizes[1]), agg[0], agg[1],
+                                                    agg[2], agg[3]);
+    dev_->set_bcast_routing(route.min_bytes, route.below_bytes);
+  }
+  if (debug_ || rank_ == 0) {
+    utils::HandleLogInfo(
+        "[xrabit] broadcast calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B "
+        "rccl %.1f us direct %.1f us -> direct %s%zu B%s\n",
+        GetWorldSize(), sizes[0], agg[0] * 1e6, agg[2] * 1e6, sizes[1], agg[1] * 1e6, agg[3] * 1e6,
+        !flags[1] ? "off (failed verification) " : (dev_->bcast_below_bytes() > 0 ? "below " : "from "),
+        dev_->bcast_below_bytes() > 0 ? dev_->bcast_below_bytes() : dev_->bcast_min_bytes(),
+        dev_->bcast_min_bytes() == static_cast<size_t>(-1) && dev_->bcast_below_bytes() == 0
+            ? " (never)" : "");
   }
   return Status::kSuccess;
 }

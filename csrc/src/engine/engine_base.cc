@@ -111,6 +111,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   }
   if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
   if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
+  if (is("rabit_device_bcast_chunk")) dcfg_.bcast_chunk = core::ParseUnit(name, val);
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
   if (is("rabit_rccl_tune")) rccl_tune_ = utils::StringToBool(val);
   if (is("rabit_rccl_init_timeout_sec")) dcfg_.comm_init_timeout_sec = atof(val);
@@ -776,6 +777,14 @@ std::string EngineBase::StatsJson() const {
      << ",\"calib_us\":[" << calib_.rccl_small * 1e6 << "," << calib_.rccl_big * 1e6 << ","
      << calib_.direct_small * 1e6 << "," << calib_.direct_big * 1e6 << "]"
      << ",\"calib_push_us\":" << calib_.push_big * 1e6
+     << ",\"calib_bcast_us\":[" << calib_bcast_[0] * 1e6 << "," << calib_bcast_[1] * 1e6 << ","
+     << calib_bcast_[2] * 1e6 << "," << calib_bcast_[3] * 1e6 << "]"
+     << ",\"bcast_routed\":" << (dev_ && dev_->bcast_routed() ? 1 : 0)
+     << ",\"bcast_direct_min\":"
+     << (dev_ && dev_->bcast_routed() ? static_cast<double>(dev_->bcast_min_bytes()) : -1.0)
+     << ",\"bcast_direct_below\":" << (dev_ ? dev_->bcast_below_bytes() : 0)
+     << ",\"direct_bcast_ops\":" << (dev_ ? dev_->bcast_ops() : 0)
+     << ",\"direct_bcast_chunks\":" << (dev_ ? dev_->bcast_chunks() : 0)
      << ",\"calib_forms_us\":[" << calib_form_us_[0] << "," << calib_form_us_[1] << ","
      << calib_form_us_[2] << "," << calib_form_us_[3] << "]"
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)

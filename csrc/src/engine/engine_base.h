@@ -183,6 +183,10 @@ class EngineBase : public IEngine {
   /*! \brief auto mode: time RCCL and the direct transport at two sizes, verify the direct
    *  result, and set the size from which ops go direct (collective) */
   Status CalibrateDevice();
+  /*! \brief auto mode, after CalibrateDevice: time the broadcast (root 0, result-log slot
+   *  included) on both transports at two sizes, verify the direct result, and route broadcasts
+   *  by their own crossover (collective) */
+  Status CalibrateBroadcast();
   /*! \brief collective: time the 128 MiB RCCL allreduce with RCCL's own channel count and
    *  with fixed CTA counts (rabit_rccl_tune_ctas), keep the fastest communicator */
   Status TuneRcclChannels();
@@ -272,6 +276,8 @@ class EngineBase : public IEngine {
   static constexpr int kCalibForms = 4;
   double calib_form_us_[kCalibForms]{-1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
+  /*! \brief last broadcast calibration: rccl small/big, direct small/big (s; 0 = not run) */
+  double calib_bcast_[4]{0, 0, 0, 0};
   bool mock_rccl_fail_{false};  // test hook: the RCCL communicator never comes up
   int rccl_failed_{0};
   bool rccl_tune_{false};          // rabit_rccl_tune: time RCCL channel counts at start-up

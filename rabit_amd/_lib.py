@@ -39,6 +39,35 @@ def load(lib: str = "standard") -> ctypes.CDLL:
     return dll
 
 
+def source_hash(root: str = None) -> str:
+    """sha256 of every library source under csrc/ (.cc, .h, .hip) concatenated in byte order of
+    their paths: the value the Makefile compiles into RabitBuildInfo"""
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    paths = []
+    for d, _, files in os.walk(os.path.join(root, "csrc")):
+        for f in files:
+            if f.endswith((".cc", ".h", ".hip")):
+                paths.append(os.path.relpath(os.path.join(d, f), root))
+    h = hashlib.sha256()
+    for p in sorted(paths, key=lambda s: s.encode()):
+        with open(os.path.join(root, p), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def build_info(lib: str = "standard") -> dict:
+    """what the library was built from (no init needed), plus whether it matches the sources
+    in this tree (`fresh`)"""
+    import json
+
+    info = json.loads(load(lib).RabitBuildInfo().decode())
+    info["library"] = os.path.relpath(lib_path(lib), os.path.dirname(_HERE))
+    info["fresh"] = info.get("src_sha256") == source_hash()
+    return info
+
+
 def _declare(d: ctypes.CDLL) -> None:
     c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
     c_ulong, c_double = ctypes.c_ulong, ctypes.c_double
@@ -48,6 +77,7 @@ def _declare(d: ctypes.CDLL) -> None:
         "RabitFinalize": (ctypes.c_bool, []),
         "RabitGetRingPrevRank": (c_int, []),
         "RabitGetRank": (c_int, []),
+        "RabitBuildInfo": (c_char_p, []),
         "RabitGetWorldSize": (c_int, []),
         "RabitIsDistributed": (c_int, []),
         "RabitTrackerPrint": (None, [c_char_p]),

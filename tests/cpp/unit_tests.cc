@@ -32,6 +32,7 @@
 #include "engine/routing.h"
 #include "device/device_plane.h"
 #include "device/p2p_plan.h"
+#include "device/bcast_plan.h"
 
 namespace {
 struct TestCase {
@@ -667,6 +668,124 @@ TEST(p2p_exchange_ops_pair_in_order) {
       EXPECT(locals == want_local && sends == moved);
     }
   }
+}
+
+
+// ---------------------------------------------------------------- pipelined direct broadcast
+// Simulates every rank's stage buffers (2 parities), user buffer and log slot byte by byte over
+// consecutive broadcasts (parity carried from op to op).  Rounds between two barriers form an
+// interval in which ranks may run in any order, so: a remote read must see a write made in an
+// EARLIER interval, and a write must not share an interval with a remote read of the same byte
+// (nor follow one without a barrier in between).
+namespace {
+struct BcastSim {
+  int n;
+  size_t stage;
+  std::vector<std::vector<std::vector<long long>>> st;  // [rank][parity][byte] tag
+  std::vector<std::vector<std::vector<int>>> wint;      // interval of the last write
+  std::vector<std::vector<std::vector<int>>> rint;      // latest interval of a remote read
+  int interval{0};
+  BcastSim(int n_, size_t stage_) : n(n_), stage(stage_) {
+    st.assign(n, std::vector<std::vector<long long>>(2, std::vector<long long>(stage, -1)));
+    wint.assign(n, std::vector<std::vector<int>>(2, std::vector<int>(stage, -1)));
+    rint.assign(n, std::vector<std::vector<int>>(2, std::vector<int>(stage, -1)));
+  }
+  // one broadcast of `bytes` from `root`; returns false on a hazard or wrong data
+  bool Run(size_t bytes, size_t chunk, int root, int *parity, size_t *barriers) {
+    const rabit::device::BcastPipeline plan(bytes, chunk, n, root);
+    std::vector<std::vector<long long>> user(n, std::vector<long long>(bytes, -1)), log = user;
+    std::vector<std::vector<int>> uw(n, std::vector<int>(bytes, 0)), lw = uw;
+    for (size_t i = 0; i < bytes; ++i) user[root][i] = static_cast<long long>(i);
+    bool ok = true;
+    const int base = *parity;
+    for (size_t t = 0; t < plan.rounds(); ++t) {
+      if (plan.barrier_before(t)) {
+        ++interval;
+        ++*barriers;
+      }
+      for (int r = 0; r < n; ++r) {
+        for (const auto &c : plan.Round(r, t)) {
+          const int p = rabit::device::BcastPipeline::parity(base, c.chunk);
+          if (c.off + c.bytes > plan.len(c.chunk) || c.off + c.bytes > stage) return false;
+          int nd = (c.to_stage ? 1 : 0) + (c.to_user ? 1 : 0) + (c.to_log ? 1 : 0);
+          if (nd == 0 || nd > 2) return false;  // the copy kernel stores at most two places
+          for (size_t b = 0; b < c.bytes; ++b) {
+            const size_t at = c.chunk * plan.chunk + c.off + b;
+            long long v;
+            if (c.from < 0) {
+              v = user[r][at];
+            } else {
+              v = st[c.from][p][c.off + b];
+              if (c.from != r) {
+                if (!(wint[c.from][p][c.off + b] < interval)) ok = false;  // read before barrier
+                rint[c.from][p][c.off + b] = std::max(rint[c.from][p][c.off + b], interval);
+              }
+            }
+            if (v != static_cast<long long>(at)) ok = false;  // wrong (or stale) bytes
+            if (c.to_stage) {
+              // nobody may still be reading the old content in this interval
+              if (rint[r][p][c.off + b] >= interval) ok = false;
+              st[r][p][c.off + b] = v;
+              wint[r][p][c.off + b] = interval;
+            }
+            if (c.to_user) {
+              user[r][at] = v;
+              uw[r][at] += 1;
+            }
+            if (c.to_log) {
+              log[r][at] = v;
+              lw[r][at] += 1;
+            }
+          }
+        }
+      }
+    }
+    *parity = plan.next_parity(base);
+    for (int r = 0; r < n; ++r) {
+      for (size_t i = 0; i < bytes; ++i) {
+        if (user[r][i] != static_cast<long long>(i) || log[r][i] != static_cast<long long>(i)) ok = false;
+        if (lw[r][i] != 1 || uw[r][i] != (r == root ? 0 : 1)) ok = false;  // each byte once
+      }
+    }
+    return ok;
+  }
+};
+}  // namespace
+
+TEST(bcast_pipeline_plan_delivers_without_races) {
+  using rabit::device::BcastPipeline;
+  std::mt19937 rng(5);
+  for (int n = 2; n <= 8; ++n) {
+    for (int trial = 0; trial < 40; ++trial) {
+      const size_t chunk = 256 + rng() % 3000;
+      BcastSim sim(n, chunk);
+      int parity = static_cast<int>(rng() % 2);
+      size_t barriers = 0;
+      // consecutive ops with different roots and sizes: hazards across op boundaries count too
+      for (int op = 0; op < 4; ++op) {
+        const size_t bytes = 1 + rng() % (6 * chunk);
+        const int root = static_cast<int>(rng() % n);
+        size_t nb = 0;
+        const bool ok = sim.Run(bytes, chunk, root, &parity, &nb);
+        EXPECT(ok);
+        if (!ok) {
+          fprintf(stderr, "  n=%d chunk=%zu bytes=%zu root=%d\n", n, chunk, bytes, root);
+          return;
+        }
+        const BcastPipeline plan(bytes, chunk, n, root);
+        // nchunks + 1 barriers (n = 2: the final local copy needs none)
+        EXPECT(nb == plan.nchunks + (n > 2 ? 1 : 0));
+        barriers += nb;
+      }
+      EXPECT(barriers > 0);
+    }
+  }
+  EXPECT(BcastPipeline(1000, 100, 1, 0).rounds() == 0);  // one rank: nothing to move
+  // automatic chunk: sqrt(S x 4 MiB) in 64 KiB steps, at least 1 MiB, at most a stage
+  EXPECT(BcastPipeline::AutoChunk(size_t(1) << 30, 256u << 20) == (64u << 20));
+  EXPECT(BcastPipeline::AutoChunk(64u << 20, 256u << 20) == (16u << 20));
+  EXPECT(BcastPipeline::AutoChunk(4u << 10, 256u << 20) == (1u << 20));
+  EXPECT(BcastPipeline::AutoChunk(size_t(16) << 30, 256u << 20) == (256u << 20));
 }
 
 TEST(rccl_result_classes) {

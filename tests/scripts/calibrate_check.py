@@ -47,5 +47,18 @@ assert fused in (0, world), fused
 # with a symmetric heap that has room, the calibration reads its inputs from the heap's tail
 want_heap = any(a.startswith("rabit_device_symmetric_heap=") for a in sys.argv[1:])
 assert st["calib_heap_src"] == (1 if want_heap else 0), st
+# the broadcast calibration ran after the allreduce one (both legs timed and the direct result
+# verified), its routing is the same everywhere, and broadcasts on both sides of it are correct
+bc = st["calib_bcast_us"]
+assert len(bc) == 4 and all(c > 0 for c in bc), bc
+assert st["bcast_routed"] == 1, st
+for key in ("bcast_direct_min", "bcast_direct_below"):
+    v = st[key]
+    assert rabit.allreduce(np.array([v]), rabit.MIN)[0] == rabit.allreduce(np.array([v]), rabit.MAX)[0], key
+for nbytes in (333, (5 << 20) + 1):
+    want = torch.arange(nbytes, dtype=torch.int64).remainder(241).to(torch.uint8)
+    b = want.to(dev) if rank == world - 1 else torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    rabit.broadcast_tensor(b, world - 1)
+    assert torch.equal(b.cpu(), want), nbytes
 rabit.finalize()
 print("[%d] CALIB OK thr=%s calib=%s" % (rank, thr, calib), flush=True)

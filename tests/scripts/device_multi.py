@@ -99,6 +99,20 @@ for nbytes in (5, 4096 + 1, (1 << 20) * 2 + 3):
         exp = torch.arange(nbytes, dtype=torch.int64).remainder(251).to(torch.uint8)
         assert torch.equal(b.cpu(), exp), ("broadcast", nbytes, root)
 
+# pipelined broadcasts (several chunks each) back to back with allreduces in between, roots
+# changing every op: the stage parity each op hands to the next must keep every buffer a slower
+# peer still reads intact (bcast_plan.h)
+for i in range(6):
+    root = (i * 3 + 1) % world
+    nbytes = (3 << 20) + 977 * i
+    pat = (torch.arange(nbytes, dtype=torch.int64) * (i + 3)).remainder(253).to(torch.uint8)
+    b = pat.to(dev) if rank == root else torch.zeros(nbytes, device=dev, dtype=torch.uint8)
+    rabit.broadcast_tensor(b, root)
+    assert torch.equal(b.cpu(), pat), ("pipelined broadcast", i, root)
+    a = torch.full(((3 << 19) + i,), float(rank + i), device=dev)
+    rabit.allreduce(a, rabit.SUM)
+    assert torch.all(a == float(sum(r + i for r in range(world)))).item(), ("allreduce after bcast", i)
+
 # allgather: equal slices through the Python API ...
 g = rabit.allgather(torch.full((1000,), float(rank), device=dev))
 assert torch.equal(g.cpu(), torch.arange(world).repeat_interleave(1000).float())
@@ -119,6 +133,9 @@ assert stats["device_direct"] == 1 and stats["device_rccl"] == 0, stats
 assert stats["oneshot_ops"] > 0, stats  # the small cases took the one-shot path
 fused_oneshot = not any(a == "rabit_device_fused_oneshot=0" for a in sys.argv[1:])
 assert (stats["fused_oneshots"] > 0) == fused_oneshot, stats  # ...in the form asked for
+# every broadcast above went direct, the large ones in several pipeline chunks
+assert stats["direct_bcast_ops"] >= 3 * world + 6, stats
+assert stats["direct_bcast_chunks"] > stats["direct_bcast_ops"], stats
 if "rabit_device_direct_mode=push" in sys.argv:
     assert stats["direct_push"] == 1 and stats["push_chunks"] > 0, stats
 

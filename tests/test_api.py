@@ -115,3 +115,18 @@ def test_half_precision_host(native_build, extra):
     out = "".join("".join(o) for o in job.outputs)
     assert rc == 0, out[-3000:]
     assert out.count("H16 OK") == 3, out[-3000:]
+
+
+@pytest.mark.parametrize("lib", ["standard", "base", "mock", "empty"])
+def test_libraries_match_sources(native_build, lib):
+    """every in-tree library carries the sha256 of the csrc/ sources it was built from (the
+    Makefile compiles it into RabitBuildInfo) and gfx950 device code: a library older than its
+    sources fails here instead of silently testing stale code"""
+    from rabit_amd import _lib
+
+    info = _lib.build_info(lib)
+    assert info["offload_arch"] == "gfx950", info
+    assert info["fresh"], ("rebuild with `make -j8`: %s was built from sources with sha256 %s, "
+                           "the tree has %s" % (info["library"], info["src_sha256"],
+                                                _lib.source_hash()))
+

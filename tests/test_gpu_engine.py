@@ -34,6 +34,17 @@ def rabit_dev():
     tracker.join(30)
 
 
+def test_box_libraries_match_sources():
+    """on the GPU box: the libraries the tests load were built from exactly the sources of this
+    tree (source hash compiled in), for gfx950 -- printed so the run's log records it"""
+    from rabit_amd import _lib
+
+    for lib in ("standard", "base", "mock"):
+        info = _lib.build_info(lib)
+        print("build_info", info)
+        assert info["offload_arch"] == "gfx950" and info["fresh"], info
+
+
 def test_device_plane_active(rabit_dev):
     assert rabit_dev.get_device() == 0
     x = torch.ones(4, device="cuda")
