@@ -275,6 +275,33 @@ def run_extras(rabit, torch, dev, world):
                                                if world > 1 else None)
     rabit.checkpoint(None)
     del hb
+    # the reference's own benchmark shape (test/speed_test.cc): 128 MiB float32 in HOST memory.
+    # Under torchrun large host allreduces go through HBM (rabit_host_via_device), pipelined
+    # through pinned slots (host_stager.h); at N = 1 it is the robust engine's host path.
+    phase("host buffer")
+    hn = (128 << 20) // 4
+    hx = torch.empty(hn, dtype=torch.float32)  # host memory, reduced in place (no copy)
+    hx.copy_(torch.from_numpy(((np.arange(hn, dtype=np.int64) * 7 + 13 * rabit.get_rank())
+                               % 1024).astype(np.float32)))
+    rabit.allreduce(hx, rabit.SUM)
+    host_ok = bool(np.array_equal(hx.numpy().astype(np.float64), host_reference(hn, world)))
+    th = []
+    for _ in range(3):
+        hx.fill_(1.0)
+        rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+        t0 = time.perf_counter()
+        rabit.allreduce(hx, rabit.SUM)
+        th.append(time.perf_counter() - t0)
+    t = float(rabit.allreduce(np.array([float(np.median(th))]), rabit.MAX)[0])
+    st_h = rabit.stats()
+    out["host_buffer_128MiB_ms"] = round(t * 1e3, 2)
+    out["host_buffer_128MiB_speed_MiBps"] = round((128 << 20) / t / 2 ** 20, 1)
+    out["host_buffer_check"] = host_ok
+    out["host_buffer_path"] = ("hbm pipelined" if st_h.get("host_staged_ops") else
+                               ("hbm" if world > 1 else "host"))
+    out["host_buffer_stage_threads"] = st_h.get("host_stage_threads")
+    rabit.checkpoint(None)
+    del hx
     # config 5: 256 MiB sum + checkpoint every iteration, against the sum alone
     out.update(run_config5(rabit, torch, dev))
     rabit.checkpoint(None)

@@ -221,6 +221,7 @@ DevicePlane::~DevicePlane() {
   // the caller's stream may be gone by now: drain the device instead of that stream
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
+  stager_.reset();
   peers_.reset();
   if (comm_ != nullptr) {
     ncclCommDestroy(comm_);
@@ -770,7 +771,8 @@ Status DevicePlane::WaitUntil(const Poll &poll, const FailureProbe &probe) {
       return Status::kTimeout;
     }
     // spin first: the wake-up latency after completion sits on the critical path of every op
-    if (waited * 1e6 > cfg_.spin_us) std::this_thread::sleep_for(std::chrono::microseconds(10));
+    const int spin = spin_us_override_ >= 0 ? spin_us_override_ : cfg_.spin_us;
+    if (waited * 1e6 > spin) std::this_thread::sleep_for(std::chrono::microseconds(10));
   }
 }
 
@@ -844,6 +846,59 @@ void DevicePlane::StageToDevice(void *dev, const void *host, size_t bytes) {
   core::DeviceWaitScope on_gpu;
   CheckHip(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream_), "H2D");
   CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+void DevicePlane::PrepareHostStager() {
+  if (stager_ != nullptr) return;
+  // the pool's share of the host: its threads (OMP_NUM_THREADS or the CPU affinity) divided
+  // among this host's ranks, when no count is configured
+  int threads = cfg_.host_stage_threads;
+  if (threads <= 0 && local_ranks_ > 0) threads = CopyPool::AutoThreads(local_ranks_);
+  stager_.reset(new HostStager(device_, cfg_.host_stage_chunk, threads));
+  stager_->set_single_stream(cfg_.host_stage_streams == 1);
+}
+
+std::string DevicePlane::HostStageJson() const {
+  if (stager_ == nullptr) return "{}";
+  const HostStager::Times &t = stager_->times();
+  char buf[256];
+  snprintf(buf, sizeof(buf),
+           "{\"runs\":%llu,\"total_ms\":%.3f,\"copy_in_ms\":%.3f,\"copy_out_ms\":%.3f,"
+           "\"wait_in_ms\":%.3f,\"wait_out_ms\":%.3f,\"enqueue_ms\":%.3f,\"chunk\":%zu,"
+           "\"threads\":%d,\"streams\":%d}",
+           static_cast<unsigned long long>(t.runs), t.total * 1e3, t.copy_in * 1e3,
+           t.copy_out * 1e3, t.wait_in * 1e3, t.wait_out * 1e3, t.enqueue * 1e3, stager_->chunk(),
+           stager_->threads(), stager_->single_stream() ? 1 : 3);
+  return buf;
+}
+
+Status DevicePlane::AllreduceHostStaged(void *host_out, const void *host_in, size_t count,
+                                        int dtype, int op, const FailureProbe &probe) {
+  const size_t tn = TypeBytes(dtype), bytes = count * tn;
+  char *d = static_cast<char *>(Scratch(bytes, 2));
+  PrepareHostStager();
+  host_staged_ops_ += 1;
+  HostStager::ChunkOp chunk_op = [&](size_t off, size_t len) {
+    return Allreduce(d + off, d + off, nullptr, len / tn, dtype, op, kPrepCopy, 1.0, probe);
+  };
+  // the host copies of the other chunks need the CPUs this wait would spin on: poll with
+  // short sleeps instead (a chunk takes milliseconds, the 10 us wake-up granularity is noise)
+  HostStager::EventWait wait = [&](hipEvent_t ev) {
+    spin_us_override_ = 0;
+    const Status w = WaitEvent(ev, probe);
+    spin_us_override_ = -1;
+    return w;
+  };
+  op_bytes_ = bytes;
+  const Status s = stager_->Run(host_out, host_in, bytes, tn, d, stream_, chunk_op, wait);
+  // a small tail chunk may have taken the one-kernel path, whose completion word nobody polls
+  // here (the D2H after it was waited for instead)
+  const volatile unsigned long long *word = nullptr;
+  unsigned long long epoch = 0;
+  if (peers_ != nullptr) (void)peers_->TakeDoneSignal(&word, &epoch);
+  op_bytes_ = 0;
+  if (s == Status::kSuccess) rccl_fail_streak_ = 0;
+  return s;
 }
 
 Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype,

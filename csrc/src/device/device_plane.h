@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "device/p2p_plan.h"
+#include "device/host_stager.h"
 #include "device/peer_coll.h"
 #include "net/socket.h"
 
@@ -68,6 +69,12 @@ struct DeviceConfig {
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
   size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
   size_t bcast_chunk{0};               // direct broadcast pipeline chunk (0: sqrt(S x 4 MiB))
+  // host-buffer allreduce staged through HBM (rabit_host_via_device): pipelined in chunks of
+  // this size through pinned slots (host_stager.h), or one whole copy each way (0)
+  size_t host_stage_chunk{16u << 20};
+  int host_stage_threads{0};           // memcpy threads of the staging (0: host share / local ranks)
+  int host_stage_streams{3};           // 3: H2D / collective / D2H on separate streams; 1: all on
+                                       // the plane stream
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
   int rccl_max_ctas{0};
   // RCCL communicator lifecycle: the bring-up (init and the connection
@@ -351,6 +358,22 @@ class DevicePlane {
   /*! \brief stage a host-reducer allreduce through pinned host memory */
   void StageToHost(void *host, const void *dev, size_t bytes);
   void StageToDevice(void *dev, const void *host, size_t bytes);
+  /*!
+   * \brief collective: host_out = allreduce(host_in) of host memory through HBM, pipelined
+   *        (H2D of chunk k+1, the device allreduce of chunk k and the D2H of chunk k-1 overlap;
+   *        multi-threaded copies between pageable and pinned memory).  Returns like a device
+   *        allreduce followed by Finish.
+   */
+  Status AllreduceHostStaged(void *host_out, const void *host_in, size_t count, int dtype, int op,
+                             const FailureProbe &probe);
+  uint64_t host_staged_ops() const { return host_staged_ops_; }
+  /*! \brief create the staging pipeline (pinned slots, copy threads, streams) ahead of use */
+  void PrepareHostStager();
+  int host_stage_threads() const { return stager_ ? stager_->threads() : 0; }
+  /*! \brief the staging's time split as JSON (ms over all staged ops; {} before the first) */
+  std::string HostStageJson() const;
+  /*! \brief ranks of the job on this host (sizes the staging's thread pool) */
+  void set_local_ranks(int n) { local_ranks_ = n; }
 
   // ---- device failure handling
   /*!
@@ -446,6 +469,10 @@ class DevicePlane {
   DeviceArena arena_;
   DeviceArena spill_;
   std::unique_ptr<PeerGroup> peers_;
+  std::unique_ptr<HostStager> stager_;  // created by the first staged host allreduce
+  uint64_t host_staged_ops_{0};
+  int local_ranks_{0};
+  int spin_us_override_{-1};  // >= 0: the busy-poll window of the current wait (host staging)
   SymHeapInfo heap_;
   size_t heap_used_{0};
   int force_{-1};

@@ -43,7 +43,9 @@ Status EngineBase::EnsureDeviceComm() {
   Status s = host_->RingAllgather(all.data(), rb * n, rb * rank_, rb * (rank_ + 1), rb);
   if (s != Status::kSuccess) return s;
   bool same_host = true, dup_gpu = false, all_peers = true;
+  int on_my_host = 0;
   for (int r = 0; r < n; ++r) {
+    on_my_host += std::strncmp(all[r].host, all[rank_].host, sizeof(rec.host)) == 0 ? 1 : 0;
     same_host = same_host && std::strncmp(all[r].host, all[0].host, sizeof(rec.host)) == 0;
     all_peers = all_peers && all[r].stage_bytes != 0;
     for (int q = 0; q < r; ++q) {
@@ -51,6 +53,7 @@ Status EngineBase::EnsureDeviceComm() {
                             std::strncmp(all[r].pci, all[q].pci, sizeof(rec.pci)) == 0);
     }
   }
+  dev_->set_local_ranks(on_my_host);  // the host-staging thread pool's share of this host
   // 2. direct transport: check that every visible peer GPU is reachable (peer access, link
   //    type), then map the peers' buffers; every rank must succeed (min-allreduce), otherwise
   //    the job runs on RCCL alone

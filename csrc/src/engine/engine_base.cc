@@ -112,6 +112,12 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_rccl_min_ctas")) dcfg_.rccl_min_ctas = atoi(val);
   if (is("rabit_device_calibrate_bytes")) dcfg_.calib_big = core::ParseUnit(name, val);
   if (is("rabit_device_bcast_chunk")) dcfg_.bcast_chunk = core::ParseUnit(name, val);
+  if (is("rabit_host_stage_chunk")) dcfg_.host_stage_chunk = core::ParseUnit(name, val);
+  if (is("rabit_host_stage_threads")) dcfg_.host_stage_threads = atoi(val);
+  if (is("rabit_host_stage_streams")) dcfg_.host_stage_streams = atoi(val) == 1 ? 1 : 3;
+  if (is("rabit_host_stage")) {
+    host_stage_mode_ = !strcmp(val, "auto") ? 2 : (utils::StringToBool(val) ? 1 : 0);
+  }
   if (is("rabit_rccl_max_ctas")) dcfg_.rccl_max_ctas = atoi(val);
   if (is("rabit_rccl_tune")) rccl_tune_ = utils::StringToBool(val);
   if (is("rabit_rccl_init_timeout_sec")) dcfg_.comm_init_timeout_sec = atof(val);
@@ -317,16 +323,57 @@ Status EngineBase::TryAllreduceHost(void *buf, const ReduceSpec &spec, const voi
     // large host buffer on a GPU node: stage through HBM and use the device transports (the
     // role of the reference's MPI engine: vendor collectives instead of TCP)
     device::DeviceGuard dg(dev_->device());
-    void *d = dev_->Scratch(bytes, 2);
     Status s = EnsureDeviceComm();
     if (s != Status::kSuccess) return s;
-    dev_->StageToDevice(d, src != nullptr ? src : buf, bytes);
-    stats_.n_device_ops += 1;
-    s = dev_->Allreduce(d, d, nullptr, spec.count, spec.dtype, spec.op, device::kPrepCopy, 1.0,
-                        MakeProbe());
-    if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
-    if (s != Status::kSuccess) return s;
-    dev_->StageToHost(buf, d, bytes);
+    const bool eligible = host_stage_mode_ != 0 && dcfg_.host_stage_chunk != 0 &&
+                          bytes >= 2 * dcfg_.host_stage_chunk;
+    bool pipe = eligible && (host_stage_mode_ == 1 || host_stage_pipe_);
+    const bool trial = eligible && host_stage_mode_ == 2 && host_stage_trial_ < 3;
+    if (trial) {
+      // auto: which form is faster depends on the host (memcpy threads, PCIe sharing), so time
+      // one op of each after one untimed warm-up op (first touches, first transfers); every
+      // rank sees the same op sequence, so the decision is collective
+      pipe = host_stage_trial_ == 2;
+      dev_->Scratch(bytes, 2);
+      dev_->PrepareHostStager();  // allocations outside the timed op
+    }
+    const double t0 = utils::GetTime();
+    if (pipe) {
+      // pipelined: H2D, device allreduce and D2H of consecutive chunks overlap
+      stats_.n_device_ops += 1;
+      s = dev_->AllreduceHostStaged(buf, src != nullptr ? src : buf, spec.count, spec.dtype,
+                                    spec.op, MakeProbe());
+    } else {
+      void *d = dev_->Scratch(bytes, 2);
+      dev_->StageToDevice(d, src != nullptr ? src : buf, bytes);
+      stats_.n_device_ops += 1;
+      s = dev_->Allreduce(d, d, nullptr, spec.count, spec.dtype, spec.op, device::kPrepCopy, 1.0,
+                          MakeProbe());
+      if (s == Status::kSuccess) s = dev_->Finish(MakeProbe());
+      if (s == Status::kSuccess) dev_->StageToHost(buf, d, bytes);
+    }
+    if (s != Status::kSuccess || !trial) return s;
+    if (host_stage_trial_ >= 1) {
+      host_stage_rate_[host_stage_trial_ - 1] =
+          static_cast<double>(bytes) / (utils::GetTime() - t0) / 1e9;
+    }
+    if (++host_stage_trial_ == 3) {
+      // the slowest rank's rate of each form decides, the same way everywhere
+      double inv[2] = {1.0 / host_stage_rate_[0], 1.0 / host_stage_rate_[1]};
+      s = host_->Allreduce(inv, sizeof(double), 2, coll::HostReducer(mpi::kDouble, mpi::kMax));
+      if (s != Status::kSuccess) {
+        host_stage_trial_ = 0;  // decide again after the recovery
+        return s;
+      }
+      host_stage_rate_[0] = 1.0 / inv[0];
+      host_stage_rate_[1] = 1.0 / inv[1];
+      host_stage_pipe_ = inv[1] < inv[0];
+      if (debug_ || rank_ == 0) {
+        utils::HandleLogInfo("[xrabit] host staging: whole copies %.2f GB/s, pipelined %.2f GB/s "
+                             "-> %s\n", host_stage_rate_[0], host_stage_rate_[1],
+                             host_stage_pipe_ ? "pipelined" : "whole copies");
+      }
+    }
     return Status::kSuccess;
   }
   ReduceFn red = spec.host_red;
@@ -785,6 +832,17 @@ std::string EngineBase::StatsJson() const {
      << ",\"bcast_direct_below\":" << (dev_ ? dev_->bcast_below_bytes() : 0)
      << ",\"direct_bcast_ops\":" << (dev_ ? dev_->bcast_ops() : 0)
      << ",\"direct_bcast_chunks\":" << (dev_ ? dev_->bcast_chunks() : 0)
+     << ",\"host_staged_ops\":" << (dev_ ? dev_->host_staged_ops() : 0)
+     << ",\"host_stage_threads\":" << (dev_ ? dev_->host_stage_threads() : 0)
+     << ",\"host_stage\":" << (dev_ ? dev_->HostStageJson() : std::string("{}"))
+     << ",\"host_stage_choice\":\""
+     << (host_stage_mode_ == 0 ? "whole"
+                               : (host_stage_mode_ == 1 ? "pipelined"
+                                                        : (host_stage_trial_ < 3
+                                                               ? "pending"
+                                                               : (host_stage_pipe_ ? "pipelined"
+                                                                                   : "whole"))))
+     << "\",\"host_stage_rates_GBps\":[" << host_stage_rate_[0] << "," << host_stage_rate_[1] << "]"
      << ",\"calib_forms_us\":[" << calib_form_us_[0] << "," << calib_form_us_[1] << ","
      << calib_form_us_[2] << "," << calib_form_us_[3] << "]"
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)

@@ -266,6 +266,13 @@ class EngineBase : public IEngine {
   bool device_replay_{true};       // recover HBM results with a device broadcast
   bool host_via_device_{false};     // stage large host-buffer allreduces through HBM
   size_t host_dev_min_{1u << 20};
+  // staged host allreduces of >= 2 chunks: 0 whole copies, 1 pipelined (host_stager.h),
+  // 2 auto: after one untimed warm-up op, one such op is timed whole and the next pipelined,
+  // and the faster (slowest rank's rate, agreed over the host plane) is kept for the job
+  int host_stage_mode_{2};
+  int host_stage_trial_{0};          // auto: eligible ops so far (3 = decided)
+  bool host_stage_pipe_{false};      // auto's decision
+  double host_stage_rate_[2]{0, 0};  // auto: whole / pipelined GB/s (slowest rank)
   /*! \brief last calibration: rccl small/big, direct small/big (s; direct big = the chosen
    *  variant), small/big bytes, push variant at the big size */
   struct {

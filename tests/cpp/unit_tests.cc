@@ -33,6 +33,7 @@
 #include "device/device_plane.h"
 #include "device/p2p_plan.h"
 #include "device/bcast_plan.h"
+#include "device/host_stager.h"
 
 namespace {
 struct TestCase {
@@ -786,6 +787,24 @@ TEST(bcast_pipeline_plan_delivers_without_races) {
   EXPECT(BcastPipeline::AutoChunk(64u << 20, 256u << 20) == (16u << 20));
   EXPECT(BcastPipeline::AutoChunk(4u << 10, 256u << 20) == (1u << 20));
   EXPECT(BcastPipeline::AutoChunk(size_t(16) << 30, 256u << 20) == (256u << 20));
+}
+
+TEST(copy_pool_splits_copies) {
+  // the host side of the pipelined host staging: one memcpy split over a pool of threads
+  std::mt19937 rng(3);
+  for (int threads : {1, 2, 5}) {
+    rabit::device::CopyPool pool(threads);
+    EXPECT(pool.threads() == threads);
+    for (size_t n : {size_t(0), size_t(1), size_t(4097), size_t(1) << 20, (size_t(3) << 20) + 77,
+                     (size_t(17) << 20) + 5}) {
+      std::vector<unsigned char> src(n + 3), dst(n + 3, 0xee);
+      for (auto &c : src) c = static_cast<unsigned char>(rng());
+      pool.Copy(dst.data() + 1, src.data() + 2, n);  // unaligned on both sides
+      EXPECT(std::equal(src.begin() + 2, src.begin() + 2 + n, dst.begin() + 1));
+      EXPECT(dst[0] == 0xee && dst[n + 1] == 0xee);  // nothing outside the range
+    }
+  }
+  EXPECT(rabit::device::CopyPool::AutoThreads() >= 1 && rabit::device::CopyPool::AutoThreads() <= 8);
 }
 
 TEST(rccl_result_classes) {

@@ -1,7 +1,7 @@
 """Fault tolerance of HBM collectives at world > 1 (direct transport; ranks share GPU 0).
 
-Each iteration: a device Sum allreduce, a device Max allreduce, a device broadcast, then an
-HBM checkpoint.  The mock engine kills ranks at given (rank, version, seqno, trial); the
+Each iteration: a device Sum allreduce, a device Max allreduce, a device broadcast (pipelined
+over 3 chunks), then an HBM checkpoint.  The mock engine kills ranks at given (rank, version, seqno, trial); the
 survivors' barrier kernels give up (peer hang-up seen on the TCP plane), the communicator
 epoch is rebuilt, and the restarted worker replays the missed results from the survivors'
 HBM result logs.  The final model is checked against its closed form."""
@@ -28,9 +28,11 @@ for it in range(start, ITERS):
     m = torch.arange(5, device=dev, dtype=torch.int32) * (rank + 1) + it
     rabit.allreduce(m, rabit.MAX)
     assert torch.equal(m.cpu(), torch.arange(5, dtype=torch.int32) * world + it), m
-    b = torch.full((777,), rank, device=dev, dtype=torch.uint8)
+    # 2.5 MiB with a 1 MiB stage: a pipelined broadcast of 3 chunks, so a kill at this op (seqno
+    # 2) leaves the survivors mid-pipeline, and a restarted rank gets it back by replay
+    b = torch.full(((5 << 19) + 777,), rank, device=dev, dtype=torch.uint8)
     rabit.broadcast_tensor(b, it % world)
-    assert int(b[0]) == it % world and int(b[-1]) == it % world
+    assert bool((b == it % world).all().item()), ("broadcast", it)
     w.add_(g)
     rabit.checkpoint_tensors({"w": w}, meta={"next": it + 1})
 expect = float(sum(r + it for it in range(ITERS) for r in range(world)))

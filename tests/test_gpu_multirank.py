@@ -83,10 +83,16 @@ def test_result_log_spills_to_host():
     assert sum(spill_replays) > 0 and sum(replays) > 0, out[-3000:]
 
 
-def test_host_buffers_via_device():
+@pytest.mark.parametrize("extra", [["rabit_host_stage=0"],
+                                   ["rabit_host_stage=1", "rabit_host_stage_chunk=1M",
+                                    "rabit_host_stage_threads=3"],
+                                   ["rabit_host_stage=auto", "rabit_host_stage_chunk=1M"]])
+def test_host_buffers_via_device(extra):
+    """host buffers through HBM: one whole copy each way, the pipelined stager, and the timed
+    choice between them (agreed on every rank)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("host_via_device.py", 3)
+    rc, out = _run("host_via_device.py", 3, extra)
     assert rc == 0, out[-5000:]
     assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
 

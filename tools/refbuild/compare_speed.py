@@ -18,7 +18,11 @@ Implementations:
   xrabit_inplace - xrabit's robust engine copying the input into the result log first
                (rabit_host_out_of_place=0, the reference's scheme) for A/B runs
   xrabit_via_dev - host buffers staged through HBM onto the device transports
-               (rabit_host_via_device=1; the MPI-engine role on a GPU node)
+               (rabit_host_via_device=1; the MPI-engine role on a GPU node); large ops
+               pipelined or whole as the timed choice finds faster (rabit_host_stage=auto)
+  xrabit_via_dev_whole - the same with one whole pageable copy each way (rabit_host_stage=0),
+               the round-1/2 form, for A/B runs
+  xrabit_via_dev_pipe - always pipelined (rabit_host_stage=1)
   xrabit_dev - xrabit with HBM buffers (device=1); only at world 1 unless --dev-worlds is
                given (several ranks on one GPU share its HBM: not an xGMI number)
 """
@@ -85,6 +89,10 @@ def main():
                                       "rabit_host_out_of_place=0"],
                    "xrabit_via_dev": [ours, str(args.n), str(args.nrep),
                                       "rabit_host_via_device=1"],
+                   "xrabit_via_dev_whole": [ours, str(args.n), str(args.nrep),
+                                            "rabit_host_via_device=1", "rabit_host_stage=0"],
+                   "xrabit_via_dev_pipe": [ours, str(args.n), str(args.nrep),
+                                           "rabit_host_via_device=1", "rabit_host_stage=1"],
                    "xrabit_dev": [ours, str(args.n), str(args.nrep), "device=1",
                                   "rabit_world1_fastpath=0"]}[impl]
             port += 7
