@@ -297,8 +297,9 @@ def run_extras(rabit, torch, dev, world):
     out["host_buffer_128MiB_ms"] = round(t * 1e3, 2)
     out["host_buffer_128MiB_speed_MiBps"] = round((128 << 20) / t / 2 ** 20, 1)
     out["host_buffer_check"] = host_ok
-    out["host_buffer_path"] = ("hbm pipelined" if st_h.get("host_staged_ops") else
-                               ("hbm" if world > 1 else "host"))
+    # N > 1: through HBM, whole copies or pipelined as the job's timed choice found (the first
+    # ops of the job are that choice's warm-up and samples)
+    out["host_buffer_path"] = ("hbm, %s" % st_h.get("host_stage_choice") if world > 1 else "host")
     out["host_buffer_stage_threads"] = st_h.get("host_stage_threads")
     rabit.checkpoint(None)
     del hx
