@@ -50,13 +50,27 @@ int CopyPool::AutoThreads(int local) {
   return std::min(8, std::max(1, HostShare() / local));
 }
 
-bool CopyPool::TakePiece() {
-  const int p = next_.fetch_add(1, std::memory_order_relaxed);
-  if (p >= pieces_) return false;
-  const size_t lo = static_cast<size_t>(p) * piece_;
-  const size_t hi = std::min(n_, lo + piece_);
-  if (hi > lo) std::memcpy(dst_ + lo, src_ + lo, hi - lo);
-  done_.fetch_add(1, std::memory_order_release);
+bool CopyPool::TakePiece(uint64_t gen) {
+  char *dst;
+  const char *src;
+  size_t lo, hi;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (gen != gen_ || next_ >= pieces_) return false;
+    const int p = next_++;
+    lo = static_cast<size_t>(p) * piece_;
+    hi = std::min(n_, lo + piece_);
+    dst = dst_;
+    src = src_;
+  }
+  // pieces are >= 64 KiB: two lock round trips per piece are noise next to the memcpy
+  if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+  bool last;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    last = ++done_ == pieces_;
+  }
+  if (last) done_cv_.notify_all();
   return true;
 }
 
@@ -69,7 +83,7 @@ void CopyPool::Work() {
       if (stop_) return;
       seen = gen_;
     }
-    while (TakePiece()) {
+    while (TakePiece(seen)) {
     }
   }
 }
@@ -81,6 +95,7 @@ void CopyPool::Copy(void *dst, const void *src, size_t n) {
     std::memcpy(dst, src, n);
     return;
   }
+  uint64_t gen;
   {
     std::lock_guard<std::mutex> lk(mu_);
     dst_ = static_cast<char *>(dst);
@@ -89,14 +104,15 @@ void CopyPool::Copy(void *dst, const void *src, size_t n) {
     // 2 pieces per thread, 64 KiB aligned, so a late-waking helper does not hold up the rest
     piece_ = ((n + 2 * t - 1) / (2 * t) + (64u << 10) - 1) / (64u << 10) * (64u << 10);
     pieces_ = static_cast<int>((n + piece_ - 1) / piece_);
-    next_.store(0, std::memory_order_relaxed);
-    done_.store(0, std::memory_order_relaxed);
-    ++gen_;
+    next_ = 0;
+    done_ = 0;
+    gen = ++gen_;
   }
   cv_.notify_all();
-  while (TakePiece()) {
+  while (TakePiece(gen)) {
   }
-  while (done_.load(std::memory_order_acquire) < pieces_) std::this_thread::yield();
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&]() { return done_ == pieces_; });
 }
 
 // ---------------------------------------------------------------- HostStager

@@ -30,7 +30,6 @@
 
 #include <hip/hip_runtime_api.h>
 
-#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <functional>
@@ -61,19 +60,22 @@ class CopyPool {
   static int AutoThreads(int local = 0);
 
  private:
+  /*! \brief the job of generation `gen`: copy its next piece; false when that job has no
+   *  piece left or a newer job replaced it (a helper waking late never touches a newer job
+   *  with an older job's pointers, and never counts a piece twice) */
+  bool TakePiece(uint64_t gen);
   void Work();
-  bool TakePiece();
   std::vector<std::thread> workers_;
   std::mutex mu_;
-  std::condition_variable cv_;
+  std::condition_variable cv_;       // workers: a new job (or stop)
+  std::condition_variable done_cv_;  // the caller: the last piece of its job is done
   bool stop_{false};
   uint64_t gen_{0};
-  // the current job
+  // the current job (all under mu_)
   char *dst_{nullptr};
   const char *src_{nullptr};
   size_t n_{0}, piece_{0};
-  int pieces_{0};
-  std::atomic<int> next_{0}, done_{0};
+  int pieces_{0}, next_{0}, done_{0};
 };
 
 class HostStager {

@@ -807,6 +807,29 @@ TEST(copy_pool_splits_copies) {
   EXPECT(rabit::device::CopyPool::AutoThreads() >= 1 && rabit::device::CopyPool::AutoThreads() <= 8);
 }
 
+TEST(copy_pool_back_to_back_jobs) {
+  // jobs follow each other with no gap, alternating sizes and buffers: a helper that wakes late
+  // for one job must neither copy with its pointers into the next nor count a piece of it twice
+  // (either would let Copy return before every byte of its job has landed)
+  rabit::device::CopyPool pool(6);
+  std::mt19937 rng(11);
+  std::vector<std::vector<unsigned char>> src(3), dst(3);
+  const size_t sizes[3] = {(size_t(1) << 20) + 4096, (size_t(5) << 20) + 3, size_t(2) << 20};
+  for (int b = 0; b < 3; ++b) {
+    src[b].resize(sizes[b]);
+    dst[b].resize(sizes[b]);
+  }
+  bool ok = true;
+  for (int it = 0; it < 300 && ok; ++it) {
+    const int b = it % 3;
+    const unsigned char v = static_cast<unsigned char>(rng());
+    std::fill(src[b].begin(), src[b].end(), v);
+    pool.Copy(dst[b].data(), src[b].data(), sizes[b]);
+    ok = std::all_of(dst[b].begin(), dst[b].end(), [v](unsigned char c) { return c == v; });
+  }
+  EXPECT(ok);
+}
+
 TEST(rccl_result_classes) {
   using rabit::device::ClassifyRccl;
   using rabit::device::RcclOutcome;
