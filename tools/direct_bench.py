@@ -24,7 +24,7 @@ def main():
     sym = os.environ.get("XR_SYM", "0") == "1"
     fused = os.environ.get("XR_FUSED", "1")
     timing = os.environ.get("XR_PHASE", "0")
-    rabit.init(sys.argv[1:], lib="base", rabit_device=0, rabit_device_phase_timing=timing,
+    rabit.init(sys.argv[1:], lib=os.environ.get("XR_LIB", "base"), rabit_device=0, rabit_device_phase_timing=timing,
                rabit_device_algo="direct", rabit_device_fused=fused,
                **({"rabit_device_symmetric_heap": "160M"} if sym else {}))
     rank, world = rabit.get_rank(), rabit.get_world_size()
