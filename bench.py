@@ -165,6 +165,13 @@ def reference_measured(world, value):
     return None
 
 
+def calibrated_mode(st):
+    """the direct form the calibration chose, as set_device_transport names it"""
+    if st.get("direct_pipeline"):
+        return "pipelined"
+    return "push" if st.get("direct_push") else "pull"
+
+
 def size_sweep(rabit, torch, dev, world):
     """N > 1: float32 sum latency from 4 KiB to 16 MiB on each transport that is up (median of
     10, ranks in lock step, max over ranks) -- the data behind the size routing; the calibrated
@@ -177,7 +184,7 @@ def size_sweep(rabit, torch, dev, world):
         up = rabit.set_device_transport(which, None)
         if which == rabit.TRANSPORT_DIRECT and up:
             # the calibrated direct form
-            up = rabit.set_device_transport(which, "push" if st0.get("direct_push") else "pull",
+            up = rabit.set_device_transport(which, calibrated_mode(st0),
                                             bool(st0.get("direct_fused")))
         up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
         if not up:
@@ -192,7 +199,7 @@ def size_sweep(rabit, torch, dev, world):
         rabit.checkpoint(None)
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
     if st0.get("device_direct"):
-        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
                                    bool(st0.get("direct_fused")))
     return out
 
@@ -223,7 +230,7 @@ def run_extras(rabit, torch, dev, world):
             phase("broadcast %s" % name)
             up = rabit.set_device_transport(which, None)
             if which == rabit.TRANSPORT_DIRECT and up:
-                up = rabit.set_device_transport(which, "push" if st0.get("direct_push") else "pull",
+                up = rabit.set_device_transport(which, calibrated_mode(st0),
                                                 bool(st0.get("direct_fused")))
             up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
             if not up:
@@ -237,7 +244,7 @@ def run_extras(rabit, torch, dev, world):
             rabit.checkpoint(None)
         rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
         if st0.get("device_direct"):
-            rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+            rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
                                        bool(st0.get("direct_fused")))
         out["broadcast_1GiB_by_transport"] = per
         st1 = rabit.stats()
@@ -402,6 +409,8 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=Fals
         for fused in (False, True):
             variants.append(("direct-%s-%s" % (mode, "fused" if fused else "classic"),
                              rabit.TRANSPORT_DIRECT, mode, fused))
+    # the push of chunk k and the gather of chunk k-2 in one round (opposite link directions)
+    variants.append(("direct-push-pipelined", rabit.TRANSPORT_DIRECT, "pipelined", False))
     st0 = rabit.stats()
     for input_name, x in bufs:
         for name, which, mode, fused in variants:
@@ -447,7 +456,7 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=Fals
         return out, phases
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
     if st0.get("device_direct"):
-        rabit.set_device_transport(rabit.TRANSPORT_AUTO, "push" if st0.get("direct_push") else "pull",
+        rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
                                    bool(st0.get("direct_fused")))
     return out, phases
 
@@ -603,11 +612,14 @@ def main():
                       "direct_min_bytes": st.get("device_direct_min", -1),
                       "direct_below_bytes": st.get("device_direct_below", 0),
                       "calibration_us": st.get("calib_us"),
-                      "direct_variant": "push" if st.get("direct_push") else "pull",
+                      "direct_variant": calibrated_mode(st),
                       "calibration_push_us": st.get("calib_push_us"),
                       "calibration_forms_us": dict(zip(
-                          ["pull-classic", "pull-fused", "push-classic", "push-fused"],
+                          ["pull-classic", "pull-fused", "push-classic", "push-fused",
+                           "push-pipelined"],
                           st.get("calib_forms_us", []))),
+                      "direct_pipeline": bool(st.get("direct_pipeline", 0)),
+                      "pipelined_ops": st.get("pipelined_ops", 0),
                       "direct_fused": bool(st.get("direct_fused", 0)),
                       "fused_chunks": st.get("fused_chunks", 0),
                       "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),

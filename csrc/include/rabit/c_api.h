@@ -105,7 +105,8 @@ RABIT_DLL void *RabitDevSymmetricAlloc(size_t nbytes);
 /*!
  * \brief benchmarking / diagnosis: route device collectives of this rank over one transport
  *        (which: -1 calibrated choice, 0 RCCL, 1 direct) and pick the direct reduce-scatter
- *        variant (direct_mode: 0 unchanged, 1 pull, 2 push).  Every rank must make the same
+ *        variant (direct_mode: 0 unchanged, 1 pull, 2 push, 3 pipelined push: the push of one
+ *        chunk and the gather of an older one share a round).  Every rank must make the same
  *        call between the same collectives.  -1 when the transport is not up.
  */
 RABIT_DLL int RabitDevSetTransport(int which, int direct_mode);

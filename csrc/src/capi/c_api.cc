@@ -279,7 +279,11 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode) {
   if (which == 1 && !d->has_peers()) return -1;
   if (direct_mode != 0 && !d->has_peers()) return -1;
   d->ForceTransport(which);
-  if (direct_mode != 0) d->SetDirectPush(direct_mode == 2);
+  if (direct_mode != 0) {
+    // 1 pull, 2 push, 3 the pipelined push form
+    d->SetDirectPush(direct_mode >= 2);
+    d->SetPipeline(direct_mode == 3);
+  }
   return 0;
 }
 

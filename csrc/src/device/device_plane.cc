@@ -658,6 +658,10 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
     peers_->set_done_signal(cfg_.done_word);
     peers_->set_bcast_chunk(cfg_.bcast_chunk);
+    // pipelined push form: forced on (with push), or off until the calibration decides
+    peers_->set_pipeline(cfg_.pipeline_mode == 1);
+    peers_->set_pipeline_chunk(cfg_.pipeline_chunk);
+    peers_->set_defer_second(cfg_.defer_second);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();

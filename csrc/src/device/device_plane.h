@@ -69,6 +69,12 @@ struct DeviceConfig {
   size_t fused_min_bytes{0};           // chunks below this keep the classic 5-launch form
   size_t calib_big{128u << 20};        // large calibration point (bytes, at most a stage)
   size_t bcast_chunk{0};               // direct broadcast pipeline chunk (0: sqrt(S x 4 MiB))
+  int pipeline_mode{2};                // direct two-shot as the pipelined push form (ar_plan.h):
+                                       // 0 never, 1 always (with push), 2 as the calibration
+                                       // finds faster
+  size_t pipeline_chunk{0};            // its chunk in bytes (0: ArPipeline::AutoChunk)
+  bool defer_second{true};             // multi-chunk ops: the second destination only after
+                                       // the last barrier (0: test knob, the old behaviour)
   // host-buffer allreduce staged through HBM (rabit_host_via_device): pipelined in chunks of
   // this size through pinned slots (host_stager.h), or one whole copy each way (0)
   size_t host_stage_chunk{16u << 20};
@@ -276,6 +282,17 @@ class DevicePlane {
   }
   bool direct_push() const { return peers_ != nullptr && peers_->push(); }
   uint64_t push_chunks() const { return peers_ ? peers_->push_chunks() : 0; }
+  /*! \brief direct two-shot allreduces as the pipelined push form (with SetDirectPush(true)) */
+  void SetPipeline(bool v) {
+    if (peers_ != nullptr) peers_->set_pipeline(v);
+  }
+  bool pipeline() const { return peers_ != nullptr && peers_->pipeline(); }
+  uint64_t pipelined_ops() const { return peers_ ? peers_->pipelined_ops() : 0; }
+  uint64_t pipelined_rounds() const { return peers_ ? peers_->pipelined_rounds() : 0; }
+  /*! \brief test hook (mock_die_mid): the next multi-chunk direct allreduce exits mid-op */
+  void ArmDieMidOp() {
+    if (peers_ != nullptr) peers_->ArmDieMidOp();
+  }
   /*! \brief barrier deadline of the direct transport (calibration runs with a short one) */
   void SetPeerDeadline(double sec) {
     if (peers_ != nullptr) peers_->set_deadline_sec(sec);

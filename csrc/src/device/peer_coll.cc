@@ -7,8 +7,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
+#include "device/ar_plan.h"
 #include "device/bcast_plan.h"
 #include "device/device_plane.h"
 #include "device/kernels.h"
@@ -38,10 +40,11 @@ inline void SegRange(size_t c, size_t seg, int p, size_t *lo, size_t *hi) {
   *hi = std::min(c, *lo + seg);
 }
 
-void AddSeg(CopyBatch *b, char *dst, const char *src, char *dst2, size_t bytes) {
+void AddSeg(CopyBatch *b, char *dst, const char *src, char *dst2, size_t bytes,
+            bool remote = false) {
   if (bytes == 0) return;
   utils::Assert(b->n < kMaxCopySegs, "copy batch overflow");
-  b->seg[b->n++] = CopySeg{dst, src, dst2, bytes};
+  b->seg[b->n++] = CopySeg{dst, src, dst2, bytes, remote ? 1 : 0};
 }
 
 /*! \brief the (at most two) byte ranges of a wrapping slice [begin, begin+size) mod total */
@@ -264,12 +267,24 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
   bool did_fused = false;
   done_pending_ = false;
+  // pipelined push form (ar_plan.h): ops above the one-shot size, raw inputs
+  if (pipeline_ && push_ && n_ >= 2 && stage_prep == kPrepCopy &&
+      !(indirect && count * tn <= oneshot_max_)) {
+    return AllreducePipelined(in, out, out2, count, tn, post_scale ? alpha : 0.0, step);
+  }
+  // A second destination (the robust engine's user buffer) may only change once the op has
+  // succeeded on this rank, so that a retry after a failure still finds the input there.  The
+  // gather of the LAST chunk follows the op's last barrier and stores it in the same pass; the
+  // chunks before it are gathered into `out` alone and copied over after the loop, by a copy the
+  // group's failure word guards (it does nothing if any barrier of the op gave up).
+  const size_t last_off = count == 0 || !defer_second_ ? 0 : (count - 1) / chunk * chunk;
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
     const int which = parity_;
     parity_ ^= 1;
     char *mine = stage(rank_, which);
     const char *chunk_src = in + off * tn;
+    char *out2_now = off >= last_off ? out2 : nullptr;  // second destination in this chunk
     // zero copy: an input in the symmetric heap is read in place by the peers (its location
     // goes out in this rank's mailbox; each rank decides for itself).  A floating-point scale
     // (gradient averaging) is applied once after the sum on every rank, so inputs stay raw.
@@ -286,7 +301,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
                            InHeap(chunk_src, c * tn) &&
                            (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
     char *chunk_out = out + off * tn;
-    char *chunk_out2 = out2 != nullptr ? out2 + off * tn : nullptr;
+    char *chunk_out2 = out2_now != nullptr ? out2_now + off * tn : nullptr;
     // every input of this decision is the same on all ranks (the kernel copes with this rank's
     // unaligned buffers itself), so all ranks run the same form of the chunk
     if (fused_ && !oneshot && builtin_op >= 0 && c * tn >= fused_min_bytes_) {
@@ -448,6 +463,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       }
       if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
       XRABIT_TRY_HIP(Barrier());
+      if (die_mid_ && off > 0) DieMidOp();  // as below, for the pull form
       XRABIT_TRY_HIP(mark(2));
       if (hi > lo) {
         const void *srcs[kMaxPeers];
@@ -465,7 +481,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
         SegRange(c, seg, p, &plo, &phi);
         const size_t at = (off + plo) * tn;
         AddSeg(&b, out + at, stage(p, which) + (static_cast<size_t>(p) * seg) * tn,
-               out2 != nullptr ? out2 + at : nullptr, (phi - plo) * tn);
+               out2_now != nullptr ? out2_now + at : nullptr, (phi - plo) * tn);
       }
       XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
       XRABIT_TRY_HIP(mark(5));
@@ -488,6 +504,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     } else {
       XRABIT_TRY_HIP(Barrier());
     }
+    // every peer passed this barrier with the previous chunk gathered into its output
+    if (die_mid_ && off > 0) DieMidOp();
     XRABIT_TRY_HIP(mark(2));
     if (hi > lo) {
       const void *srcs[kMaxPeers];
@@ -505,13 +523,89 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     for (int p = 0; p < n_; ++p) {
       SegRange(c, seg, p, &lo, &hi);
       const size_t at = (off + lo) * tn;
-      AddSeg(&b, out + at, stage(p, which) + lo * tn, out2 != nullptr ? out2 + at : nullptr,
+      AddSeg(&b, out + at, stage(p, which) + lo * tn, out2_now != nullptr ? out2_now + at : nullptr,
              (hi - lo) * tn);
     }
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     XRABIT_TRY_HIP(mark(5));
   }
+  if (out2 != nullptr && last_off > 0) {
+    // the chunks before the last into the second destination, only if every barrier held
+    CopyBatch b;
+    NewBatch(&b);
+    AddSeg(&b, out2, out, nullptr, last_off * tn);
+    XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+  }
   timing_pending_ = timed && !did_fused;  // phases exist only in the classic form
+  return hipSuccess;
+}
+
+void PeerGroup::DieMidOp() {
+  die_mid_ = false;
+  (void)hipStreamSynchronize(stream_);
+  fprintf(stderr, "[%d]@@@Hit Mock Die Mid Op: exiting inside a multi-chunk device allreduce\n",
+          rank_);
+  fflush(stderr);
+  std::_Exit(kMockDieMidExitCode);
+}
+
+hipError_t PeerGroup::AllreducePipelined(const char *in, char *out, char *out2, size_t count,
+                                         size_t tn, double post, const ReduceStep &step) {
+  const size_t chunk =
+      pipeline_chunk_ != 0
+          ? std::max<size_t>(256 * static_cast<size_t>(n_),
+                             pipeline_chunk_ / tn / (256 * static_cast<size_t>(n_)) *
+                                 (256 * static_cast<size_t>(n_)))
+          : ArPipeline::AutoChunk(count, tn, n_, stage_bytes_);
+  const ArPipeline plan(count, chunk, n_);
+  utils::Check(plan.stage_bytes(tn) <= stage_bytes_,
+               "pipelined allreduce: a chunk of %zu elements needs %zu stage bytes, %zu available",
+               chunk, plan.stage_bytes(tn), stage_bytes_);
+  const int base = parity_;
+  for (size_t t = 0; t < plan.rounds(); ++t) {
+    // pushes of chunk t (remote writes) and gathers of chunk t-2 (remote reads) in one launch:
+    // opposite directions of every link
+    CopyBatch b;
+    NewBatch(&b);
+    for (const ArCopy &c : plan.Copies(rank_, t)) {
+      const int p = ArPipeline::parity(base, c.chunk);
+      const size_t at = (c.chunk * plan.chunk + c.lo) * tn;
+      const size_t bytes = (c.hi - c.lo) * tn;
+      if (c.push) {
+        AddSeg(&b, stage(c.peer, p) + plan.inbox(rank_) * tn, in + at, nullptr, bytes, true);
+      } else {
+        char *second = out2 != nullptr && (plan.second_in_gather(c.chunk) || !defer_second_)
+                           ? out2 + at
+                           : nullptr;
+        AddSeg(&b, out + at, stage(c.peer, p) + plan.result() * tn, second, bytes);
+      }
+    }
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    // the reduce of chunk t-1: this rank's n inbox slots into its result slot
+    const ArReduce red = plan.Reduce(rank_, t);
+    if (red.any) {
+      char *mine = stage(rank_, ArPipeline::parity(base, red.chunk));
+      const void *srcs[kMaxPeers];
+      for (int s = 0; s < n_; ++s) srcs[s] = mine + plan.inbox(s) * tn;
+      XRABIT_TRY_HIP(step(mine + plan.result() * tn, srcs, n_, red.hi - red.lo, dev_status(),
+                          nullptr, post, stream_));
+    }
+    if (plan.barrier_after(t)) {
+      XRABIT_TRY_HIP(Barrier());
+      // after round 2's barrier every peer has gathered chunk 0 into its output
+      if (die_mid_ && t >= 2 && plan.nchunks >= 2) DieMidOp();
+    }
+    ++pipelined_rounds_;
+  }
+  if (out2 != nullptr && plan.second_tail() > 0 && defer_second_) {
+    CopyBatch b;
+    NewBatch(&b);
+    AddSeg(&b, out2, out, nullptr, plan.second_tail() * tn);
+    XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+  }
+  parity_ = plan.next_parity(base);
+  ++pipelined_ops_;
+  push_chunks_ += plan.nchunks;
   return hipSuccess;
 }
 

@@ -47,6 +47,8 @@ constexpr int kMaxCopySegs = 16;
 /*! \brief bytes of the flag area at the start of each exported allocation: kMaxPeers arrival
  *  flags at offset 0, the local failure word at kPeerStatusOffset */
 constexpr size_t kPeerFlagBytes = 64 * 1024;
+/*! \brief exit status of a rank leaving through the mock_die_mid hook (the launcher restarts it) */
+constexpr int kMockDieMidExitCode = 250;
 constexpr size_t kPeerStatusOffset = 4096;
 /*! \brief two mailbox words (by stage parity): where this rank's input of the current chunk
  *  lives, published before the first barrier of the chunk (see ResolveArgs) */
@@ -63,13 +65,15 @@ struct CopySeg {
   const char *src;
   char *dst2;  // optional second destination (nullptr: none)
   size_t bytes;
+  int remote;  // 1: dst is a peer's memory (push): system-scope write-through stores, dst
+               // 16-byte aligned, no dst2
 };
 
 struct CopyBatch {
   CopySeg seg[kMaxCopySegs];
   int n;
   const int *guard;  // optional device word: the launch does nothing when it is non-zero
-  int remote;        // 1: every dst is a peer's memory (push): system-scope write-through stores
+  int remote;        // 1: every segment is remote (as CopySeg::remote)
 };
 
 /*!
@@ -261,6 +265,27 @@ class PeerGroup {
   uint64_t push_chunks() const { return push_chunks_; }
   uint64_t oneshot_ops() const { return oneshot_ops_; }
   /*!
+   * \brief two-shot allreduces as the PIPELINED push form (ar_plan.h): the push reduce-scatter
+   *        of chunk k (outgoing links) and the gather of chunk k-2 (incoming links) share a
+   *        round, one barrier per round.  Applies with set_push(true) to ops above the one-shot
+   *        size; the calibration times it as a form of its own.
+   */
+  void set_pipeline(bool v) { pipeline_ = v; }
+  bool pipeline() const { return pipeline_; }
+  /*! \brief bytes per pipeline chunk (0: ArPipeline::AutoChunk) */
+  void set_pipeline_chunk(size_t bytes) { pipeline_chunk_ = bytes; }
+  uint64_t pipelined_ops() const { return pipelined_ops_; }
+  uint64_t pipelined_rounds() const { return pipelined_rounds_; }
+  /*!
+   * \brief test hook (mock_die_mid): the next multi-chunk allreduce exits the process in the
+   *        middle, right after a barrier that every peer passed only with the op's first chunk
+   *        already gathered into its output, so survivors fail the op with part of it delivered
+   */
+  void ArmDieMidOp() { die_mid_ = true; }
+  /*! \brief test knob (rabit_device_defer_second=0): store the second destination in every
+   *  chunk's gather, as before the deferral, to show what the deferral protects */
+  void set_defer_second(bool v) { defer_second_ = v; }
+  /*!
    * \brief two-shot chunks of built-in ops run as ONE fused kernel (per-tile flags, see
    *        FusedAllreduceArgs) instead of stage + barrier + reduce + barrier + gather launches
    */
@@ -313,6 +338,11 @@ class PeerGroup {
   hipError_t AllreduceImpl(const void *send, void *recv, void *recv2, size_t count, size_t tn,
                            int dtype, int prep, double alpha, const ReduceStep &step,
                            bool indirect, bool op_is_sum = false, int builtin_op = -1);
+  /*! \brief the pipelined push form of AllreduceImpl (ar_plan.h) */
+  hipError_t AllreducePipelined(const char *in, char *out, char *out2, size_t count, size_t tn,
+                                double post, const ReduceStep &step);
+  /*! \brief mock_die_mid: wait for the stream, then leave the process (see ArmDieMidOp) */
+  void DieMidOp();
   /*! \brief true if [p, p + bytes) lies in this rank's symmetric heap */
   bool InHeap(const void *p, size_t bytes) const {
     const char *c = static_cast<const char *>(p);
@@ -362,6 +392,11 @@ class PeerGroup {
   uint64_t oneshot_ops_{0};
   bool push_{false};
   uint64_t push_chunks_{0};
+  bool pipeline_{false};
+  size_t pipeline_chunk_{0};
+  uint64_t pipelined_ops_{0}, pipelined_rounds_{0};
+  bool die_mid_{false};
+  bool defer_second_{true};
   bool fused_{true};
   size_t fused_oneshot_max_{64u << 10};
   uint64_t fused_oneshots_{0};

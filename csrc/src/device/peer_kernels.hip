@@ -14,7 +14,9 @@
  *
  * Copy batch: up to kMaxCopySegs (dst, src[, dst2]) segments in one launch; workgroup b takes
  * tile b / nseg of segment b % nseg, so the workgroups in flight read from every peer at once
- * and all xGMI links carry traffic together.  Tiles are 256 lanes x 16 B (kUnroll = 1: 4 KiB per
+ * and all xGMI links carry traffic together.  Remote segments (pushes into a peer's memory) may
+ * share a launch with pulls: the pipelined allreduce sends one chunk out while it gathers an
+ * older one in, over both directions of every link at once.  Tiles are 256 lanes x 16 B (kUnroll = 1: 4 KiB per
  * workgroup), like the other streaming kernels (kernels.hip).
  */
 #include <hip/hip_runtime.h>
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
   const size_t lo = tile * kTileBytes;
   if (lo >= g.bytes) return;
   const size_t hi = std::min(g.bytes, lo + kTileBytes);
-  if (batch.remote) {
+  if (batch.remote || g.remote) {
     PushTile(g, lo, hi);
     return;
   }
@@ -199,9 +201,12 @@ hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsign
 
 hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream) {
   if (batch.n < 0 || batch.n > kMaxCopySegs) return hipErrorInvalidValue;
-  for (int i = 0; i < batch.n && batch.remote; ++i) {
+  for (int i = 0; i < batch.n; ++i) {
     // push destinations are whole-16-byte inbox slots (PushTile pads the last word)
-    if (!Al16(batch.seg[i].dst) || batch.seg[i].dst2 != nullptr) return hipErrorInvalidValue;
+    if ((batch.remote || batch.seg[i].remote) &&
+        (!Al16(batch.seg[i].dst) || batch.seg[i].dst2 != nullptr)) {
+      return hipErrorInvalidValue;
+    }
   }
   size_t tiles = 0;
   for (int i = 0; i < batch.n; ++i) {

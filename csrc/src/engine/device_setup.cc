@@ -303,23 +303,30 @@ Status EngineBase::CalibrateDevice() {
   //     of the 5-launch one (or the reverse).  A failed run disables the direct transport
   //     altogether (a failed barrier drops the group); a wrong result only rules that form out.
   //     Variant 0 is the form step 1 measured.
+  //     Form 4 is the pipelined push form (ar_plan.h: the push of one chunk and the gather of
+  //     an older one share a round, over opposite link directions), timed when
+  //     rabit_device_pipeline=auto; with rabit_device_pipeline=1 every push form is pipelined.
   const bool fused_auto = dcfg_.fused_mode == 2;
   const bool cfg_fused = dcfg_.fused_mode == 1;  // auto starts from the classic form
+  const bool pipe_on = dcfg_.pipeline_mode == 1;
   struct Form {
-    bool push, fused;
+    bool push, fused, pipe;
   };
-  Form forms[kCalibForms] = {{dcfg_.direct_mode == 2, cfg_fused},
-                             {dcfg_.direct_mode == 2, !cfg_fused},
-                             {true, cfg_fused},
-                             {true, !cfg_fused}};
-  int form_ok[kCalibForms] = {ok, 0, 0, 0};
-  double t_form[kCalibForms] = {t[1][1], 0, 0, 0};
+  Form forms[kCalibForms] = {{dcfg_.direct_mode == 2, cfg_fused, dcfg_.direct_mode == 2 && pipe_on},
+                             {dcfg_.direct_mode == 2, !cfg_fused, dcfg_.direct_mode == 2 && pipe_on},
+                             {true, cfg_fused, pipe_on},
+                             {true, !cfg_fused, pipe_on},
+                             {true, false, true}};
+  int form_ok[kCalibForms] = {ok, 0, 0, 0, 0};
+  double t_form[kCalibForms] = {t[1][1], 0, 0, 0, 0};
   const bool try_push = dcfg_.direct_mode == 0;
   for (int f = 1; f < kCalibForms && ok; ++f) {
     if ((f == 1 || f == 3) && !fused_auto) continue;
     if (f >= 2 && !try_push) continue;
+    if (f == 4 && dcfg_.pipeline_mode != 2) continue;
     dev_->SetDirectPush(forms[f].push);
     dev_->SetFused(forms[f].fused);
+    dev_->SetPipeline(forms[f].pipe);
     Status st;
     if (!measure(1, 1, &st)) {
       ok = 0;
@@ -332,17 +339,20 @@ Status EngineBase::CalibrateDevice() {
     for (size_t i = 0; i < sizes[1] && form_ok[f]; ++i) form_ok[f] = host[i] == want ? 1 : 0;
     if (!form_ok[f]) {
       utils::HandleLogInfo("[%d] direct %s %s verification failed\n", rank_,
-                           forms[f].push ? "push" : "pull", forms[f].fused ? "fused" : "classic");
+                           forms[f].push ? "push" : "pull",
+                           forms[f].pipe ? "pipelined" : (forms[f].fused ? "fused" : "classic"));
     }
   }
   t[1][1] = t_form[0];
   if (dev_->has_peers()) {
     dev_->SetDirectPush(forms[0].push);
     dev_->SetFused(forms[0].fused);
+    dev_->SetPipeline(forms[0].pipe);
   }
   dev_->ForceTransport(-1);
   dev_->SetPeerDeadline(dcfg_.peer_deadline_sec);
-  int flags[1 + kCalibForms] = {ok, form_ok[0], form_ok[1], form_ok[2], form_ok[3]};
+  int flags[1 + kCalibForms] = {ok};
+  for (int f = 0; f < kCalibForms; ++f) flags[1 + f] = form_ok[f];
   Status s = host_->Allreduce(flags, sizeof(int), 1 + kCalibForms,
                               coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
@@ -360,8 +370,8 @@ Status EngineBase::CalibrateDevice() {
     dev_->ForceTransport(-1);
   }
   // identical decision everywhere: max time over ranks
-  double agg[4 + kCalibForms] = {t[0][0], t[0][1], t[1][0], t[1][1],
-                                 t_form[0], t_form[1], t_form[2], t_form[3]};
+  double agg[4 + kCalibForms] = {t[0][0], t[0][1], t[1][0], t[1][1]};
+  for (int f = 0; f < kCalibForms; ++f) agg[4 + f] = t_form[f];
   s = host_->Allreduce(agg, sizeof(double), 4 + kCalibForms,
                        coll::HostReducer(mpi::kDouble, mpi::kMax));
   if (s != Status::kSuccess) return s;
@@ -377,6 +387,7 @@ Status EngineBase::CalibrateDevice() {
     }
     dev_->SetDirectPush(forms[best].push);
     dev_->SetFused(forms[best].fused);
+    dev_->SetPipeline(forms[best].pipe);
     agg[3] = agg[4 + best];
     // linear model t = a + b * bytes per transport through the two points (routing.h)
     const DirectRouting route =
@@ -392,10 +403,12 @@ Status EngineBase::CalibrateDevice() {
   if (debug_ || rank_ == 0) {
     utils::HandleLogInfo(
         "[xrabit] device calibration (%d ranks): %zu B rccl %.1f us direct %.1f us; %zu B rccl "
-        "%.1f us direct %.1f us (%s %s; forms %.1f %.1f %.1f %.1f us) -> direct %s\n",
+        "%.1f us direct %.1f us (%s %s; forms %.1f %.1f %.1f %.1f %.1f us) -> direct %s\n",
         n, sizes[0] * 4, agg[0] * 1e6, agg[2] * 1e6, sizes[1] * 4, agg[1] * 1e6, agg[3] * 1e6,
-        dev_->direct_push() ? "push" : "pull", forms[best].fused ? "fused" : "classic",
+        dev_->direct_push() ? "push" : "pull",
+        forms[best].pipe ? "pipelined" : (forms[best].fused ? "fused" : "classic"),
         calib_form_us_[0], calib_form_us_[1], calib_form_us_[2], calib_form_us_[3],
+        calib_form_us_[4],
         !ok ? "disabled (failed verification)"
             : (threshold != static_cast<size_t>(-1)
                    ? ("from " + std::to_string(threshold) + " B").c_str()

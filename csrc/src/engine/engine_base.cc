@@ -133,10 +133,19 @@ void EngineBase::SetParam(const char *name, const char *val) {
       dcfg_.direct_mode = 1;
     } else if (!strcmp(val, "push")) {
       dcfg_.direct_mode = 2;
+    } else if (!strcmp(val, "pipelined")) {
+      dcfg_.direct_mode = 2;  // the pipelined form is a push form
+      dcfg_.pipeline_mode = 1;
     } else {
-      utils::Error("rabit_device_direct_mode must be auto, pull or push (got %s)", val);
+      utils::Error("rabit_device_direct_mode must be auto, pull, push or pipelined (got %s)", val);
     }
   }
+  if (is("rabit_device_pipeline")) {
+    // auto: the calibration times the pipelined push form against the others
+    dcfg_.pipeline_mode = !strcmp(val, "auto") ? 2 : (utils::StringToBool(val) ? 1 : 0);
+  }
+  if (is("rabit_device_pipeline_chunk")) dcfg_.pipeline_chunk = core::ParseUnit(name, val);
+  if (is("rabit_device_defer_second")) dcfg_.defer_second = utils::StringToBool(val);
   if (is("rabit_device_symmetric_heap")) dcfg_.sym_heap = core::ParseUnit(name, val);
   if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
@@ -844,7 +853,10 @@ std::string EngineBase::StatsJson() const {
                                                                                    : "whole"))))
      << "\",\"host_stage_rates_GBps\":[" << host_stage_rate_[0] << "," << host_stage_rate_[1] << "]"
      << ",\"calib_forms_us\":[" << calib_form_us_[0] << "," << calib_form_us_[1] << ","
-     << calib_form_us_[2] << "," << calib_form_us_[3] << "]"
+     << calib_form_us_[2] << "," << calib_form_us_[3] << "," << calib_form_us_[4] << "]"
+     << ",\"direct_pipeline\":" << (dev_ && dev_->pipeline() ? 1 : 0)
+     << ",\"pipelined_ops\":" << (dev_ ? dev_->pipelined_ops() : 0)
+     << ",\"pipelined_rounds\":" << (dev_ ? dev_->pipelined_rounds() : 0)
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"rccl_init_failed\":" << rccl_failed_

@@ -199,8 +199,13 @@ class EngineBase : public IEngine {
   bool PeerFailureProbe() const;
   /*! \brief Hadoop status line */
   void ReportStatus() const;
-  /*! \brief mock_dev_hang: wedge this rank's stream before the next device collective */
+  /*! \brief mock_dev_hang: wedge this rank's stream before the next device collective;
+   *  mock_die_mid: leave the process in the middle of the next multi-chunk direct allreduce */
   void MaybeInjectDeviceHang() {
+    if (die_mid_armed_) {
+      die_mid_armed_ = false;
+      dev_->ArmDieMidOp();
+    }
     if (!dev_hang_armed_) return;
     dev_hang_armed_ = false;
     dev_->InjectHang(dev_hang_max_sec_);
@@ -280,8 +285,9 @@ class EngineBase : public IEngine {
   } calib_{0, 0, 0, 0, 0, 0, 0};
   /*! \brief forms of the direct two-shot path the calibration times at its large size:
    *  {configured, other fused/classic, push configured-fused, push other}; us, -1 = not run */
-  static constexpr int kCalibForms = 4;
-  double calib_form_us_[kCalibForms]{-1, -1, -1, -1};
+  // forms of the direct two-shot path: pull / push x classic / fused, and the pipelined push
+  static constexpr int kCalibForms = 5;
+  double calib_form_us_[kCalibForms]{-1, -1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
   /*! \brief last broadcast calibration: rccl small/big, direct small/big (s; 0 = not run) */
   double calib_bcast_[4]{0, 0, 0, 0};
@@ -292,6 +298,7 @@ class EngineBase : public IEngine {
   std::string rccl_tune_ctas_{"64,112"};  // candidate CTA counts besides RCCL's own choice
   std::string rccl_tune_json_{"{}"};      // what the tuning measured (stats)          // epochs whose RCCL communicator did not come up on every rank
   bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
+  bool die_mid_armed_{false};      // set by the mock engine's mock_die_mid
   double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long
   double dev_wait_limit_sec_{600};  // watchdog: a wait on this rank's GPU may last this long
   bool trace_spans_{false};

@@ -11,7 +11,10 @@
  * forever) instead of dying, to exercise the timeout watchdog; `mock_dev_hang=...` keeps the
  * process alive but wedges its GPU stream right before the device collective (a hung kernel:
  * the peers' barriers / RCCL time out, the rank finds its own stream stuck after the abort and
- * exits for a restart); `force_local` and `report_stats` behave as in the reference.
+ * exits for a restart); `mock_die_mid=...` lets the rank start the device allreduce and exit
+ * in its middle, once every peer has delivered the op's first chunk to its output (survivors
+ * then fail the op part-way, which must leave their input intact for the retry); `force_local`
+ * and `report_stats` behave as in the reference.
  */
 #ifndef XRABIT_ENGINE_ENGINE_MOCK_H_
 #define XRABIT_ENGINE_ENGINE_MOCK_H_
@@ -39,12 +42,16 @@ class EngineMock : public EngineRobust {
     }
     if (!strcmp(name, "report_stats")) report_stats_ = atoi(val);
     if (!strcmp(name, "force_local")) force_local_ = atoi(val);
-    if (!strcmp(name, "mock") || !strcmp(name, "mock_hang") || !strcmp(name, "mock_dev_hang")) {
+    if (!strcmp(name, "mock") || !strcmp(name, "mock_hang") || !strcmp(name, "mock_dev_hang") ||
+        !strcmp(name, "mock_die_mid")) {
       Key k;
       utils::Check(sscanf(val, "%d,%d,%d,%d", &std::get<0>(k), &std::get<1>(k), &std::get<2>(k),
                           &std::get<3>(k)) == 4,
                    "invalid mock parameter \"%s\" (expected rank,version,seqno,ntrial)", val);
-      mock_map_[k] = !strcmp(name, "mock_hang") ? 2 : (!strcmp(name, "mock_dev_hang") ? 3 : 1);
+      mock_map_[k] = !strcmp(name, "mock_hang")       ? 2
+                     : !strcmp(name, "mock_dev_hang") ? 3
+                     : !strcmp(name, "mock_die_mid")  ? 4
+                                                      : 1;
     }
   }
   const char *EngineName() const override { return "mock"; }
@@ -173,6 +180,12 @@ class EngineMock : public EngineRobust {
     auto it = mock_map_.find(Key(rank_, version_number_, seq_counter_, num_trial_));
     if (it == mock_map_.end()) return;
     num_trial_ += 1;
+    if (it->second == 4) {
+      fprintf(stderr, "[%d]@@@Hit Mock Die Mid (armed):%s\n", rank_, what);
+      fflush(stderr);
+      die_mid_armed_ = true;
+      return;
+    }
     if (it->second == 3) {
       // the process stays alive and responsive on the host; its GPU stream wedges right before
       // this collective, so its peers wait at the device barrier / in RCCL for it

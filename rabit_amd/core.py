@@ -435,12 +435,14 @@ def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str]
                          fused: Optional[bool] = None) -> bool:
     """Route this rank's device collectives over one transport (benchmarks / diagnosis):
     TRANSPORT_AUTO (the calibrated choice), TRANSPORT_RCCL or TRANSPORT_DIRECT, pick the
-    direct reduce-scatter variant ("pull" / "push") and the form of the direct two-shot path
-    (fused=True: one kernel per chunk with per-tile hand-offs; False: the 5-launch form).
+    direct reduce-scatter variant ("pull" / "push" / "pipelined": push whose rounds also carry
+    the gather of an older chunk, over the opposite link direction) and the form of the direct
+    two-shot path (fused=True: one kernel per chunk with per-tile hand-offs; False: the 5-launch
+    form).
     Every rank must make the same call between the same collectives.  False when that
     transport is not up on this rank."""
     _check_init()
-    mode = {None: 0, "pull": 1, "push": 2}[direct_mode]
+    mode = {None: 0, "pull": 1, "push": 2, "pipelined": 3}[direct_mode]
     if _LIB.RabitDevSetTransport(int(which), mode) != 0:
         return False
     if fused is not None:

@@ -33,6 +33,7 @@
 #include "device/device_plane.h"
 #include "device/p2p_plan.h"
 #include "device/bcast_plan.h"
+#include "device/ar_plan.h"
 #include "device/host_stager.h"
 
 namespace {
@@ -787,6 +788,140 @@ TEST(bcast_pipeline_plan_delivers_without_races) {
   EXPECT(BcastPipeline::AutoChunk(64u << 20, 256u << 20) == (16u << 20));
   EXPECT(BcastPipeline::AutoChunk(4u << 10, 256u << 20) == (1u << 20));
   EXPECT(BcastPipeline::AutoChunk(size_t(16) << 30, 256u << 20) == (256u << 20));
+}
+
+// Pipelined two-shot allreduce (ar_plan.h), simulated element by element over consecutive ops
+// (parity carried from op to op).  Every stage element carries a tag (element index, mask of the
+// ranks summed into it).  Rules, for accesses by ANY rank (the owner's own reduce included):
+// a read must see a write from an EARLIER barrier interval, and a write must not share its
+// interval with another access of the same element (nor the op boundary, which has no barrier).
+namespace {
+struct ArSim {
+  int n;
+  size_t stage;  // elements per parity
+  std::vector<std::vector<std::vector<long long>>> st;  // [rank][parity][elem] tag
+  std::vector<std::vector<std::vector<int>>> wint, rint;
+  int interval{0};
+  ArSim(int n_, size_t stage_) : n(n_), stage(stage_) {
+    st.assign(n, std::vector<std::vector<long long>>(2, std::vector<long long>(stage, -1)));
+    wint.assign(n, std::vector<std::vector<int>>(2, std::vector<int>(stage, -1)));
+    rint = wint;
+  }
+  static long long Tag(size_t idx, int mask) { return static_cast<long long>(idx) * 256 + mask; }
+  bool Read(int owner, int p, size_t e, long long *v) {
+    if (e >= stage || !(wint[owner][p][e] < interval)) return false;
+    rint[owner][p][e] = std::max(rint[owner][p][e], interval);
+    *v = st[owner][p][e];
+    return true;
+  }
+  bool Write(int owner, int p, size_t e, long long v) {
+    if (e >= stage || rint[owner][p][e] >= interval || wint[owner][p][e] >= interval) return false;
+    st[owner][p][e] = v;
+    wint[owner][p][e] = interval;
+    return true;
+  }
+  // one allreduce of `count` elements; false on a hazard or a wrong result
+  bool Run(size_t count, size_t chunk, int *parity, size_t *barriers) {
+    const rabit::device::ArPipeline plan(count, chunk, n);
+    if (plan.stage_bytes(1) > stage) return false;
+    const int full = (1 << n) - 1;
+    std::vector<std::vector<long long>> out(n, std::vector<long long>(count, -1)), second = out;
+    std::vector<std::vector<int>> ow(n, std::vector<int>(count, 0)), sw = ow;
+    const int base = *parity;
+    bool ok = true;
+    for (size_t t = 0; t < plan.rounds() && ok; ++t) {
+      for (int r = 0; r < n && ok; ++r) {
+        for (const auto &c : plan.Copies(r, t)) {
+          const int p = rabit::device::ArPipeline::parity(base, c.chunk);
+          for (size_t j = 0; j < c.hi - c.lo && ok; ++j) {
+            const size_t at = c.chunk * plan.chunk + c.lo + j;
+            if (c.push) {
+              ok = Write(c.peer, p, plan.inbox(r) + j, Tag(at, 1 << r));
+            } else {
+              long long v = -1;
+              ok = Read(c.peer, p, plan.result() + j, &v) && v == Tag(at, full);
+              out[r][at] = v;
+              ow[r][at] += 1;
+              if (plan.second_in_gather(c.chunk)) {
+                second[r][at] = v;
+                sw[r][at] += 1;
+              }
+            }
+          }
+        }
+        const rabit::device::ArReduce red = plan.Reduce(r, t);
+        if (red.any) {
+          const int p = rabit::device::ArPipeline::parity(base, red.chunk);
+          for (size_t j = 0; j < red.hi - red.lo && ok; ++j) {
+            const size_t at = red.chunk * plan.chunk + red.lo + j;
+            int mask = 0;
+            for (int s = 0; s < n && ok; ++s) {
+              long long v = -1;
+              ok = Read(r, p, plan.inbox(s) + j, &v) && v == Tag(at, 1 << s);
+              mask |= 1 << s;
+            }
+            ok = ok && Write(r, p, plan.result() + j, Tag(at, mask));
+          }
+        }
+      }
+      if (plan.barrier_after(t)) {
+        ++interval;
+        ++*barriers;
+      }
+    }
+    // the guarded tail copy after the last round
+    for (int r = 0; r < n; ++r) {
+      for (size_t i = 0; i < plan.second_tail(); ++i) {
+        second[r][i] = out[r][i];
+        sw[r][i] += 1;
+      }
+    }
+    *parity = plan.next_parity(base);
+    for (int r = 0; r < n && ok; ++r) {
+      for (size_t i = 0; i < count; ++i) {
+        if (out[r][i] != Tag(i, full) || second[r][i] != Tag(i, full)) ok = false;
+        if (ow[r][i] != 1 || sw[r][i] != 1) ok = false;
+      }
+    }
+    return ok;
+  }
+};
+}  // namespace
+
+TEST(allreduce_pipeline_plan_reduces_without_races) {
+  using rabit::device::ArPipeline;
+  std::mt19937 rng(9);
+  for (int n = 2; n <= 8; ++n) {
+    for (int trial = 0; trial < 30; ++trial) {
+      const size_t chunk = 256 * static_cast<size_t>(n) * (1 + rng() % 4);
+      const ArPipeline probe(chunk, chunk, n);
+      ArSim sim(n, probe.stage_bytes(1));
+      int parity = static_cast<int>(rng() % 2);
+      size_t barriers = 0;
+      // consecutive ops of different sizes: hazards across op boundaries count too
+      for (int op = 0; op < 3; ++op) {
+        const size_t count = 1 + rng() % (chunk * 5);
+        size_t nb = 0;
+        const bool ok = sim.Run(count, chunk, &parity, &nb);
+        EXPECT(ok);
+        if (!ok) {
+          fprintf(stderr, "  n=%d chunk=%zu count=%zu op=%d\n", n, chunk, count, op);
+          return;
+        }
+        const ArPipeline plan(count, chunk, n);
+        EXPECT(nb == plan.nchunks + 1);  // one barrier per round but the last
+        barriers += nb;
+      }
+      EXPECT(barriers > 0);
+    }
+  }
+  // automatic chunk: sqrt(S x 4 MiB), >= 1 MiB, a multiple of 256 n elements, within the stage
+  const size_t c128 = ArPipeline::AutoChunk((128u << 20) / 4, 4, 8, 256u << 20);
+  EXPECT(c128 % (256 * 8) == 0 && c128 * 4 >= (22u << 20) && c128 * 4 <= (24u << 20));
+  EXPECT(ArPipeline(c128, c128, 8).stage_bytes(4) <= (256u << 20));
+  const size_t cbig = ArPipeline::AutoChunk(size_t(4) << 30, 4, 8, 256u << 20);
+  EXPECT(ArPipeline(cbig, cbig, 8).stage_bytes(4) <= (256u << 20));
+  EXPECT(ArPipeline::AutoChunk(1024, 4, 2, 256u << 20) == (1u << 20) / 4);
 }
 
 TEST(copy_pool_splits_copies) {

@@ -33,13 +33,16 @@ assert below == 0 or thr >= 2 ** 63, (below, thr)
 assert st["calib_push_us"] > 0, st
 push = rabit.allreduce(np.array([st["direct_push"]]), rabit.SUM)[0]
 assert push in (0, world), push
-# the forms of the two-shot path were timed and verified (pull/push x classic; the fused forms
-# too with rabit_device_fused=auto), and the chosen form is the same everywhere
+# the forms of the two-shot path were timed and verified (pull/push x classic and the pipelined
+# push form; the fused forms too with rabit_device_fused=auto), and the chosen form is the same
+# everywhere
 forms = st["calib_forms_us"]
 fused_auto = "rabit_device_fused=auto" in sys.argv[1:]
-assert len(forms) == 4 and forms[0] > 0 and forms[2] > 0, forms
+assert len(forms) == 5 and forms[0] > 0 and forms[2] > 0 and forms[4] > 0, forms
+pipe = rabit.allreduce(np.array([st["direct_pipeline"]]), rabit.SUM)[0]
+assert pipe in (0, world), pipe
 if fused_auto:
-    assert all(f > 0 for f in forms), forms
+    assert all(f > 0 for f in forms[:4]), forms
 else:
     assert forms[1] == -1 and forms[3] == -1 and st["direct_fused"] == 0, (forms, st)
 fused = rabit.allreduce(np.array([st["direct_fused"]]), rabit.SUM)[0]

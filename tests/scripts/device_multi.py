@@ -138,6 +138,10 @@ assert stats["direct_bcast_ops"] >= 3 * world + 6, stats
 assert stats["direct_bcast_chunks"] > stats["direct_bcast_ops"], stats
 if "rabit_device_direct_mode=push" in sys.argv:
     assert stats["direct_push"] == 1 and stats["push_chunks"] > 0, stats
+if "rabit_device_direct_mode=pipelined" in sys.argv:
+    # the two-shot ops went through the pipelined push form, several rounds each
+    assert stats["direct_pipeline"] == 1 and stats["direct_push"] == 1, stats
+    assert stats["pipelined_ops"] > 0 and stats["pipelined_rounds"] > 3 * stats["pipelined_ops"], stats
 
 # a rough number for the log: 64 MiB fp32 sum, all ranks' traffic on the one shared GPU
 x = torch.ones(16 << 20, device=dev)

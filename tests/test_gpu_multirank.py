@@ -34,24 +34,33 @@ def test_direct_collectives(world, fused):
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
 
+# the pipelined push form with 256 KiB chunks: the suite's 3 MiB ops take several rounds
+PIPELINED = ["rabit_device_direct_mode=pipelined", "rabit_device_pipeline_chunk=256K"]
+
+
+@pytest.mark.parametrize("mode", ["push", "pipelined"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_direct_collectives_push(world):
-    """the push (remote-write) reduce-scatter variant of the two-shot allreduce"""
+def test_direct_collectives_push(world, mode):
+    """the push (remote-write) reduce-scatter variant of the two-shot allreduce, and its
+    pipelined form (the push of chunk k and the gather of chunk k-2 in one round, ar_plan.h)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("device_multi.py", world, ["rabit_device_direct_mode=push"])
+    rc, out = _run("device_multi.py", world,
+                   PIPELINED if mode == "pipelined" else ["rabit_device_direct_mode=push"])
     assert rc == 0, out[-5000:]
     assert out.count("DEVMULTI OK") == world, out[-3000:]
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("mock", [[], ["mock=1,1,0,0"], ["mock=0,2,1,0", "mock=2,1,2,0"]])
-@pytest.mark.parametrize("mode", ["pull", "push"])
+@pytest.mark.parametrize("mode", ["pull", "push", "pipelined"])
 def test_direct_recovery(mock, mode, fused):
-    """kills at fixed points, both forms of the two-shot path (fused=1: the survivors' fused
+    """kills at fixed points, every form of the two-shot path (fused=1: the survivors' fused
     kernels give up on the abort word, the guard word keeps later launches of the group idle)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if mode == "pipelined" and fused == "1":
+        pytest.skip("the pipelined form has no fused variant")
     rc, out = _run("device_ft.py", 3, mock + ["rabit_device_direct_mode=" + mode,
                                               "rabit_device_fused=" + fused,
                                               "rabit_device_fused_oneshot=" + fused], attempts=4)
@@ -64,6 +73,23 @@ def test_direct_recovery(mock, mode, fused):
         import re
         replays = [int(x) for x in re.findall(r"DEVFT OK replays=(\d+)", out)]
         assert sum(replays) > 0, out[-3000:]
+
+
+@pytest.mark.parametrize("mode", ["pull", "push", "pipelined"])
+def test_death_inside_multi_chunk_allreduce(mode):
+    """mock_die_mid: rank 1 leaves in the middle of a multi-chunk device allreduce, after every
+    peer has gathered the op's first chunk.  The survivors fail the op part-way; their user
+    buffers must still hold the inputs (the chunks before the last reach the user buffer only
+    through a copy guarded by the group's failure word), or the retry would sum partial results
+    and the final model would miss its closed form."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("device_ft.py", 3, ["mock_die_mid=1,1,0,0", "rabit_device_direct_mode=" + mode,
+                                       "rabit_device_fused=0"], attempts=3)
+    assert rc == 0, out[-5000:]
+    assert out.count("DEVFT OK") == 3, out[-3000:]
+    assert "Hit Mock Die Mid Op" in out, out[-3000:]
+    assert "resumed at version" in out, out[-3000:]
 
 
 def test_result_log_spills_to_host():
@@ -157,7 +183,8 @@ def test_bench_torchrun_shared_gpu(n):
     ran = [v for v in rec["variants"] if v["available"]]
     assert {(v["transport"], v["input"]) for v in ran} >= {
         ("direct-%s-%s" % (m, f), i) for m in ("pull", "push") for f in ("classic", "fused")
-        for i in ("torch", "symmetric")}, rec["variants"]
+        for i in ("torch", "symmetric")} | {
+        ("direct-push-pipelined", i) for i in ("torch", "symmetric")}, rec["variants"]
     assert all(v["check"] and v["t_us"] > 0 for v in ran), rec["variants"]
     # where the classic direct form's time goes, per phase, for pull and push
     br = {b["transport"]: b for b in rec["direct_phase_breakdown"]}
@@ -168,7 +195,7 @@ def test_bench_torchrun_shared_gpu(n):
         assert all(t >= 0 for t in b["phase_us"].values()) and b["phase_us"]["gather"] > 0, b
 
 
-@pytest.mark.parametrize("mode", ["pull", "push"])
+@pytest.mark.parametrize("mode", ["pull", "push", "pipelined"])
 def test_direct_half_precision(mode):
     """bf16 / fp16 allreduce (sum, max, min, fused averaging) on HBM through the direct
     transport: fp32 accumulation over all ranks, one rounding, bit-exact against torch"""

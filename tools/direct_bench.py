@@ -67,6 +67,8 @@ def main():
                 "fused": fused == "1", "fused_chunks": st.get("fused_chunks", 0),
                 "fused_oneshots": st.get("fused_oneshots", 0),
                 "direct_push": st.get("direct_push", 0),
+                "direct_pipeline": st.get("direct_pipeline", 0),
+                "pipelined_ops": st.get("pipelined_ops", 0),
                 "phase_us": phase, "timed_ops": n1 - n0,
             }), flush=True)
         del x
