@@ -276,8 +276,11 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // succeeded on this rank, so that a retry after a failure still finds the input there.  The
   // gather of the LAST chunk follows the op's last barrier and stores it in the same pass; the
   // chunks before it are gathered into `out` alone and copied over after the loop, by a copy the
-  // group's failure word guards (it does nothing if any barrier of the op gave up).
+  // group's failure word guards (it does nothing if any barrier of the op gave up).  The fused
+  // kernels hand tiles over one by one, with no last barrier: a peer dying inside one leaves some
+  // tiles delivered and others not, so they never store the second destination themselves.
   const size_t last_off = count == 0 || !defer_second_ ? 0 : (count - 1) / chunk * chunk;
+  size_t tail_end = last_off;  // [0, tail_end) reaches out2 through the guarded copy
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
     const int which = parity_;
@@ -315,7 +318,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       }
       fa.src = chunk_src;
       fa.out = chunk_out;
-      fa.out2 = chunk_out2;
+      fa.out2 = defer_second_ ? nullptr : chunk_out2;
+      if (defer_second_ && chunk_out2 != nullptr) tail_end = off + c;
       fa.count = c;
       fa.seg = seg;
       // about one tile per workgroup of the grid, 8-64 KiB, a multiple of 256 elements
@@ -360,7 +364,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       }
       fa.src = chunk_src;
       fa.out = chunk_out;
-      fa.out2 = chunk_out2;
+      fa.out2 = defer_second_ ? nullptr : chunk_out2;
+      if (defer_second_ && chunk_out2 != nullptr) tail_end = off + c;
       fa.count = c;
       // 4 KiB tiles (at least 256 elements; larger when the op needs more than the flag
       // slots): up to 64 workgroups for the default largest one-shot op (256 KiB)
@@ -529,11 +534,12 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     XRABIT_TRY_HIP(mark(5));
   }
-  if (out2 != nullptr && last_off > 0) {
-    // the chunks before the last into the second destination, only if every barrier held
+  if (out2 != nullptr && tail_end > 0) {
+    // the chunks before the last (and fused chunks) into the second destination, only if every
+    // barrier and hand-off of the op held
     CopyBatch b;
     NewBatch(&b);
-    AddSeg(&b, out2, out, nullptr, last_off * tn);
+    AddSeg(&b, out2, out, nullptr, tail_end * tn);
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
   }
   timing_pending_ = timed && !did_fused;  // phases exist only in the classic form
