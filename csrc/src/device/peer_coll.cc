@@ -270,6 +270,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // pipelined push form (ar_plan.h): ops above the one-shot size, raw inputs
   if (pipeline_ && push_ && n_ >= 2 && stage_prep == kPrepCopy &&
       !(indirect && count * tn <= oneshot_max_)) {
+    timing_pending_ = false;  // no phase events in this form
     return AllreducePipelined(in, out, out2, count, tn, post_scale ? alpha : 0.0, step);
   }
   // A second destination (the robust engine's user buffer) may only change once the op has
