@@ -209,6 +209,14 @@ def run_extras(rabit, torch, dev, world):
     (result log and checkpoint paths included, as in the headline step)."""
     out = {}
     if world > 1:
+        # xGMI per-link and all-link bandwidth, reads / writes / both ways (direct transport's
+        # IPC mappings; on ranks sharing one GPU this is HBM): min over ranks
+        phase("link probe")
+        lp = rabit.link_probe(64 << 20)
+        if lp is not None:
+            keys = sorted(lp)
+            low = rabit.allreduce(np.array([lp[k] for k in keys]), rabit.MIN)
+            out["link_probe_min_over_ranks"] = {k: round(float(v), 2) for k, v in zip(keys, low)}
         out["size_sweep"] = size_sweep(rabit, torch, dev, world)
     # config 3: Broadcast of a 1 GiB blob from root 0
     nb = 1 << 30

@@ -134,6 +134,14 @@ RABIT_DLL int RabitDevGraphAllreduce(void *buf, size_t count, int enum_dtype, in
  * \return 0, or -1 without a direct transport
  */
 RABIT_DLL int RabitDevSetPhaseTiming(int on);
+/*!
+ * \brief xGMI link probe over the direct transport (a collective outside the fault-tolerance
+ *        log: every rank calls it between the same ops).  out[0..4] (nout >= 5) receive this
+ *        rank's GB/s: one link read, one link write (every rank to rank + k at once, mean over
+ *        k), all links read, all links write, all links both directions at once.  0 on success,
+ *        -2 without a direct transport (world 1, several hosts), -1 on failure.
+ */
+RABIT_DLL int RabitDevLinkProbe(size_t nbytes, double *out, int nout);
 /*! \brief 0 (default): an error prints and exits the process (the launcher restarts it);
  *         1: an error is recorded (RabitGetLastError) and the call returns */
 RABIT_DLL void RabitSetErrorMode(int mode);

@@ -316,6 +316,12 @@ RABIT_DLL int RabitDevSetFused(int fused) {
   return 0;
 }
 
+RABIT_DLL int RabitDevLinkProbe(size_t nbytes, double *out, int nout) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || out == nullptr || nout < rabit::device::PeerGroup::kLinkProbeValues) return -1;
+  return Guard([&]() { return e->DevLinkProbe(nbytes, out); }, -1);
+}
+
 RABIT_DLL int RabitDevSetPhaseTiming(int on) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
   if (e == nullptr || e->device_plane() == nullptr) return -1;

@@ -876,6 +876,23 @@ std::string DevicePlane::HostStageJson() const {
   return buf;
 }
 
+Status DevicePlane::LinkProbe(size_t bytes, double out[PeerGroup::kLinkProbeValues]) {
+  utils::Check(peers_ != nullptr, "link probe needs the direct transport");
+  DeviceGuard dg(device_);
+  // a peer that never arrives costs seconds, not the op deadline
+  peers_->set_deadline_sec(std::min(cfg_.peer_deadline_sec, 10.0));
+  const hipError_t e = peers_->LinkProbe(bytes, out);
+  CheckHip(e, "link probe");
+  CheckHip(hipStreamSynchronize(stream_), "link probe");
+  const bool failed = peers_->failed();
+  peers_->set_deadline_sec(cfg_.peer_deadline_sec);
+  if (failed) {
+    AbortComm();
+    return Status::kAborted;
+  }
+  return Status::kSuccess;
+}
+
 Status DevicePlane::AllreduceHostStaged(void *host_out, const void *host_in, size_t count,
                                         int dtype, int op, const FailureProbe &probe) {
   const size_t tn = TypeBytes(dtype), bytes = count * tn;

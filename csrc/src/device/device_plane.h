@@ -289,6 +289,13 @@ class DevicePlane {
   bool pipeline() const { return peers_ != nullptr && peers_->pipeline(); }
   uint64_t pipelined_ops() const { return peers_ ? peers_->pipelined_ops() : 0; }
   uint64_t pipelined_rounds() const { return peers_ ? peers_->pipelined_rounds() : 0; }
+  /*!
+   * \brief xGMI link probe over the direct transport (PeerGroup::LinkProbe; a collective
+   *        outside the fault-tolerance log, every rank calls it between the same ops).  GB/s of
+   *        this rank: one link read / write, all links read / write, all links both ways.  A
+   *        failed barrier aborts the group (the next op rebuilds it) and returns kAborted.
+   */
+  Status LinkProbe(size_t bytes, double out[PeerGroup::kLinkProbeValues]);
   /*! \brief test hook (mock_die_mid): the next multi-chunk direct allreduce exits mid-op */
   void ArmDieMidOp() {
     if (peers_ != nullptr) peers_->ArmDieMidOp();

@@ -547,6 +547,76 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   return hipSuccess;
 }
 
+hipError_t PeerGroup::LinkProbe(size_t bytes, double out[kLinkProbeValues]) {
+  utils::Assert(opened_, "peer group not opened");
+  for (int i = 0; i < kLinkProbeValues; ++i) out[i] = 0;
+  if (n_ < 2) return hipSuccess;
+  const size_t total = std::max<size_t>(4096, std::min(bytes, stage_bytes_) / 4096 * 4096);
+  const size_t per = std::max<size_t>(4096, total / static_cast<size_t>(n_ - 1) / 4096 * 4096);
+  hipEvent_t e0, e1;
+  XRABIT_TRY_HIP(hipEventCreate(&e0));
+  XRABIT_TRY_HIP(hipEventCreate(&e1));
+  // sources in parity 0 of the stages, destinations in parity 1
+  auto timed = [&](const CopyBatch &b, double *ms) -> hipError_t {
+    XRABIT_TRY_HIP(Barrier());
+    XRABIT_TRY_HIP(hipEventRecord(e0, stream_));
+    XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    XRABIT_TRY_HIP(hipEventRecord(e1, stream_));
+    XRABIT_TRY_HIP(hipEventSynchronize(e1));
+    float m = 0;
+    XRABIT_TRY_HIP(hipEventElapsedTime(&m, e0, e1));
+    *ms = m;
+    return hipSuccess;
+  };
+  hipError_t err = hipSuccess;
+  double ms = 0, sum_pull = 0, sum_push = 0;
+  for (int k = 1; k < n_ && err == hipSuccess; ++k) {
+    const int to = (rank_ + k) % n_;
+    CopyBatch b;
+    NewBatch(&b);
+    AddSeg(&b, stage(rank_, 1), stage(to, 0), nullptr, total);
+    err = timed(b, &ms);
+    sum_pull += total / (ms * 1e-3) / 1e9;
+    if (err != hipSuccess) break;
+    NewBatch(&b);
+    AddSeg(&b, stage(to, 1), stage(rank_, 0), nullptr, total, true);
+    err = timed(b, &ms);
+    sum_push += total / (ms * 1e-3) / 1e9;
+  }
+  if (err == hipSuccess) {
+    out[0] = sum_pull / (n_ - 1);
+    out[1] = sum_push / (n_ - 1);
+    CopyBatch pull, push, both;
+    NewBatch(&pull);
+    NewBatch(&push);
+    NewBatch(&both);
+    for (int k = 1; k < n_; ++k) {
+      const int q = (rank_ + k) % n_;
+      // each rank writes its own slice of a peer's parity-1 stage (no two writers overlap)
+      char *remote_dst = stage(q, 1) + static_cast<size_t>(rank_) * per;
+      char *local_dst = stage(rank_, 1) + static_cast<size_t>(q) * per;
+      AddSeg(&pull, local_dst, stage(q, 0), nullptr, per);
+      AddSeg(&push, remote_dst, stage(rank_, 0), nullptr, per, true);
+      AddSeg(&both, local_dst, stage(q, 0), nullptr, per);
+      AddSeg(&both, remote_dst, stage(rank_, 0), nullptr, per, true);
+    }
+    const double moved = static_cast<double>(per) * (n_ - 1);
+    if (per * static_cast<size_t>(n_) <= stage_bytes_) {
+      err = timed(pull, &ms);
+      if (err == hipSuccess) out[2] = moved / (ms * 1e-3) / 1e9;
+      if (err == hipSuccess) err = timed(push, &ms);
+      if (err == hipSuccess) out[3] = moved / (ms * 1e-3) / 1e9;
+      if (err == hipSuccess) err = timed(both, &ms);
+      if (err == hipSuccess) out[4] = moved / (ms * 1e-3) / 1e9;
+    }
+  }
+  // nobody's next op may write a stage a peer's probe copy still touches
+  if (err == hipSuccess) err = Barrier();
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return err;
+}
+
 void PeerGroup::DieMidOp() {
   die_mid_ = false;
   (void)hipStreamSynchronize(stream_);

@@ -245,6 +245,21 @@ class PeerGroup {
    */
   hipError_t Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in);
 
+  /*!
+   * \brief xGMI link probe (a collective: every rank of the group calls it between the same
+   *        ops).  Copies of `bytes` (at most a stage) through the IPC mappings, each started
+   *        right after a barrier and timed with hipEvents on this rank:
+   *          [0] one link, reads: every rank pulls from rank + k at once, mean over k = 1..n-1
+   *          [1] one link, writes: every rank pushes to rank + k at once, mean over k
+   *          [2] all links, reads: every rank pulls bytes / (n-1) from each peer at once
+   *          [3] all links, writes: every rank pushes bytes / (n-1) to each peer at once
+   *          [4] all links, both directions: [2] and [3] in one launch (bytes each way)
+   *        out[i] = GB/s of this rank (bytes moved per direction / its time).  The stages'
+   *        contents are garbage afterwards; a barrier at the end keeps the next op's stage
+   *        writes behind every probe copy.
+   */
+  hipError_t LinkProbe(size_t bytes, double out[5]);
+  static constexpr int kLinkProbeValues = 5;
   /*! \brief make spinning barriers give up (host side; safe at any time) */
   void SignalAbort();
   /*! \brief true when a barrier gave up (read after the stream drained) */

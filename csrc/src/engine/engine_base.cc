@@ -732,6 +732,14 @@ int EngineBase::DevGraphAllreduce(void *buf, size_t count, int dtype, int op,
   return r;
 }
 
+int EngineBase::DevLinkProbe(size_t bytes, double *out) {
+  if (dev_ == nullptr || GetWorldSize() < 2) return -2;
+  device::DeviceGuard dg(dev_->device());
+  if (EnsureDeviceComm() != Status::kSuccess) return -1;
+  if (!dev_->has_peers()) return -2;
+  return dev_->LinkProbe(bytes, out) == Status::kSuccess ? 0 : -1;
+}
+
 void EngineBase::DevCheckPoint(int n, void *const *ptrs, const size_t *nbytes,
                                const std::string &meta, int nl, void *const *lptrs,
                                const size_t *lnbytes) {

@@ -104,6 +104,12 @@ class EngineBase : public IEngine {
    */
   int DevGraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream,
                         std::string *why);
+  /*!
+   * \brief xGMI link probe (DevicePlane::LinkProbe) after bringing the device transports up;
+   *        out receives 5 GB/s values of this rank.  0, -1 when it failed, -2 without a
+   *        direct transport (world 1, or ranks on several hosts).
+   */
+  int DevLinkProbe(size_t bytes, double *out);
   /*! \brief copy engine of the checkpoint host mirrors (rabit_device_mirror_engine; a
    *         rabit_device_mirror_ctas > 0 alone selects the kernel engine) */
   int MirrorEngine() const {

@@ -15,7 +15,6 @@ from .core import (BITOR, DTYPE_ENUM, DTYPE_ENUM__, MAX, MIN, PREP_ABS, PREP_COP
                    set_error_mode, stats, tracker_print, version_number, dump_trace,
                    checkpoint_tensors, load_checkpoint_tensors, symmetric_empty,
                    set_device_transport, set_phase_timing, allreduce_graphable, TRANSPORT_AUTO,
-                   TRANSPORT_DIRECT,
-                   TRANSPORT_RCCL)
+                   TRANSPORT_DIRECT, TRANSPORT_RCCL, link_probe)
 
 __version__ = "0.1.0"

@@ -450,6 +450,28 @@ def set_device_transport(which: int = TRANSPORT_AUTO, direct_mode: Optional[str]
     return True
 
 
+LINK_PROBE_KEYS = ("one_link_read_GBps", "one_link_write_GBps", "all_links_read_GBps",
+                   "all_links_write_GBps", "all_links_both_ways_GBps")
+
+
+def link_probe(nbytes: int = 64 << 20) -> Optional[dict]:
+    """xGMI link bandwidth of this rank over the direct transport's IPC mappings (a collective
+    outside the fault-tolerance log: every rank calls it between the same ops).  Copies of
+    `nbytes` (at most one stage buffer), each right after a barrier: one link read / write (every
+    rank to rank + k at once, mean over k), all links read / write (1/(n-1) of the bytes to or
+    from each peer at once), all links both ways at once.  GB/s per direction of this rank; None
+    without a direct transport (world 1, ranks on several hosts).  Raises RuntimeError if a peer
+    failed during the probe (the next collective rebuilds the transport)."""
+    _check_init()
+    out = (ctypes.c_double * 5)()
+    r = _LIB.RabitDevLinkProbe(int(nbytes), out, 5)
+    if r == -2:
+        return None
+    if r != 0:
+        raise RuntimeError("link probe failed: " + last_error())
+    return {k: round(float(v), 2) for k, v in zip(LINK_PROBE_KEYS, out)}
+
+
 def allreduce_graphable(t, op: int):
     """In-place RCCL allreduce of an HBM tensor on the current stream, with no host-side
     synchronisation: unlike allreduce(), it can be captured into a hipGraph with the rest of

@@ -92,6 +92,17 @@ def test_death_inside_multi_chunk_allreduce(mode):
     assert "resumed at version" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_link_probe(world):
+    """rabit.link_probe(): per-link and all-link copy bandwidth over the IPC mappings (xGMI on
+    separate GPUs, HBM here); the transport stays exact afterwards"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("link_probe_check.py", world)
+    assert rc == 0, out[-5000:]
+    assert out.count("LINKPROBE OK") == world, out[-3000:]
+
+
 def test_result_log_spills_to_host():
     """an HBM result log capped below one iteration's results: the entries past the cap live in
     pinned host memory, and killed ranks replay both kinds (HBM and spilled) from survivors"""
@@ -178,6 +189,8 @@ def test_bench_torchrun_shared_gpu(n):
     assert rec["value"] == rec["busbw_GBps"] and rec["value_is"] == "busbw_GBps", rec
     assert rec["transport"]["direct"] == 1, rec
     assert rec["result_check"], rec
+    if rec.get("extras"):
+        assert all(v > 0 for v in rec["extras"]["link_probe_min_over_ranks"].values()), rec["extras"]
     assert "post_headline_failure" not in rec, rec["post_headline_failure"]
     # every available transport x input variant ran and matched the host fp64 reference
     ran = [v for v in rec["variants"] if v["available"]]
