@@ -29,8 +29,9 @@
  *
  * The robust engine passes a second destination (the user buffer) that may only change once
  * the op succeeded on this rank: gathers before the last barrier store the output alone, and a
- * copy guarded by the group's failure word moves those chunks to the second destination after
- * the last round (second_tail).  The last chunk's gather follows the last barrier and stores both.
+ * copy guarded by the group's failure word moves those chunks to the second destination in the
+ * last round (second_tail), in the same launch as the last chunk's gather, which follows the
+ * last barrier and stores both.
  *
  * The op's last reads (the final gather, no barrier after it) are of parity
  * base ^ ((nchunks-1) & 1), so the next op starts on the other one, base ^ (nchunks & 1).
@@ -110,8 +111,8 @@ struct ArPipeline {
   /*! \brief the gather of chunk k may store the second destination (it follows the last
    *  barrier); earlier chunks reach it through the guarded tail copy */
   bool second_in_gather(size_t k) const { return k + 1 == nchunks; }
-  /*! \brief elements [0, second_tail()) are copied output -> second destination after the
-   *  last round (guarded: only when every barrier held) */
+  /*! \brief elements [0, second_tail()) are copied output -> second destination in the last
+   *  round, after the last barrier (guarded: only when every barrier held) */
   size_t second_tail() const { return nchunks == 0 ? 0 : (nchunks - 1) * chunk; }
 
   /*! \brief the copies `rank` makes in round t (pushes first, then gathers) */

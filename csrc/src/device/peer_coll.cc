@@ -47,6 +47,18 @@ void AddSeg(CopyBatch *b, char *dst, const char *src, char *dst2, size_t bytes,
   b->seg[b->n++] = CopySeg{dst, src, dst2, bytes, remote ? 1 : 0};
 }
 
+/*! \brief dst[0, bytes) = src[0, bytes) as equal 4 KiB-aligned segments in the batch's free
+ *  slots: a large local copy then shares a launch with a gather, and the two run at once (one
+ *  HBM-bound, the other xGMI-bound on separate GPUs) */
+void AddSplit(CopyBatch *b, char *dst, const char *src, size_t bytes) {
+  if (bytes == 0) return;
+  const size_t slots = static_cast<size_t>(std::max(1, kMaxCopySegs - b->n));
+  const size_t piece = RoundUp((bytes + slots - 1) / slots, 4096);
+  for (size_t o = 0; o < bytes; o += piece) {
+    AddSeg(b, dst + o, src + o, nullptr, std::min(piece, bytes - o));
+  }
+}
+
 /*! \brief the (at most two) byte ranges of a wrapping slice [begin, begin+size) mod total */
 int SliceRanges(size_t begin, size_t size, size_t total, size_t lo[2], size_t hi[2]) {
   if (size == 0) return 0;
@@ -489,6 +501,12 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
         AddSeg(&b, out + at, stage(p, which) + (static_cast<size_t>(p) * seg) * tn,
                out2_now != nullptr ? out2_now + at : nullptr, (phi - plo) * tn);
       }
+      if (out2_now != nullptr && tail_end > 0) {
+        // the earlier chunks into the second destination in the same launch (after the op's
+        // last barrier, guarded like the gather)
+        AddSplit(&b, out2, out, tail_end * tn);
+        tail_end = 0;
+      }
       XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
       XRABIT_TRY_HIP(mark(5));
       ++push_chunks_;
@@ -531,6 +549,10 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       const size_t at = (off + lo) * tn;
       AddSeg(&b, out + at, stage(p, which) + lo * tn, out2_now != nullptr ? out2_now + at : nullptr,
              (hi - lo) * tn);
+    }
+    if (out2_now != nullptr && tail_end > 0) {
+      AddSplit(&b, out2, out, tail_end * tn);  // as in the push form above
+      tail_end = 0;
     }
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     XRABIT_TRY_HIP(mark(5));
@@ -657,6 +679,12 @@ hipError_t PeerGroup::AllreducePipelined(const char *in, char *out, char *out2, 
         AddSeg(&b, out + at, stage(c.peer, p) + plan.result() * tn, second, bytes);
       }
     }
+    const bool final_round = t + 1 == plan.rounds();
+    if (final_round && out2 != nullptr && defer_second_) {
+      // after the last barrier: the earlier chunks into the second destination, in the launch
+      // of the last gather (local HBM copy and xGMI reads at once)
+      AddSplit(&b, out2, out, plan.second_tail() * tn);
+    }
     if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
     // the reduce of chunk t-1: this rank's n inbox slots into its result slot
     const ArReduce red = plan.Reduce(rank_, t);
@@ -673,12 +701,6 @@ hipError_t PeerGroup::AllreducePipelined(const char *in, char *out, char *out2, 
       if (die_mid_ && t >= 2 && plan.nchunks >= 2) DieMidOp();
     }
     ++pipelined_rounds_;
-  }
-  if (out2 != nullptr && plan.second_tail() > 0 && defer_second_) {
-    CopyBatch b;
-    NewBatch(&b);
-    AddSeg(&b, out2, out, nullptr, plan.second_tail() * tn);
-    XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
   }
   parity_ = plan.next_parity(base);
   ++pipelined_ops_;
