@@ -614,8 +614,9 @@ hipError_t PeerGroup::LinkProbe(size_t bytes, double out[kLinkProbeValues]) {
     NewBatch(&both);
     for (int k = 1; k < n_; ++k) {
       const int q = (rank_ + k) % n_;
-      // each rank writes its own slice of a peer's parity-1 stage (no two writers overlap)
-      char *remote_dst = stage(q, 1) + static_cast<size_t>(rank_) * per;
+      // pulls land in slices [0, n) of the puller's parity-1 stage and pushes in slices
+      // [n, 2n) of the receiver's, one slice per writer: no two writers overlap
+      char *remote_dst = stage(q, 1) + static_cast<size_t>(n_ + rank_) * per;
       char *local_dst = stage(rank_, 1) + static_cast<size_t>(q) * per;
       AddSeg(&pull, local_dst, stage(q, 0), nullptr, per);
       AddSeg(&push, remote_dst, stage(rank_, 0), nullptr, per, true);
@@ -623,7 +624,7 @@ hipError_t PeerGroup::LinkProbe(size_t bytes, double out[kLinkProbeValues]) {
       AddSeg(&both, remote_dst, stage(rank_, 0), nullptr, per, true);
     }
     const double moved = static_cast<double>(per) * (n_ - 1);
-    if (per * static_cast<size_t>(n_) <= stage_bytes_) {
+    if (per * static_cast<size_t>(2 * n_) <= stage_bytes_) {
       err = timed(pull, &ms);
       if (err == hipSuccess) out[2] = moved / (ms * 1e-3) / 1e9;
       if (err == hipSuccess) err = timed(push, &ms);

@@ -7,7 +7,7 @@ import torch
 
 import rabit_amd as rabit
 
-rabit.init(sys.argv[1:], lib="standard", rabit_device=0, rabit_device_peer_buffer="16M")
+rabit.init(sys.argv[1:], lib="standard", rabit_device=0, rabit_device_peer_buffer="32M")
 rank, world = rabit.get_rank(), rabit.get_world_size()
 dev = torch.device("cuda", 0)
 x = torch.full((1 << 20,), float(rank + 1), device=dev)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out/r3_s28"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_multirank.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "push or recovery or death or half or direct_collectives or calibration or small_op" > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_multirank.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "push or recovery or death or half or direct_collectives or calibration or small_op or link_probe" > "$OUT/pytest.log" 2>&1
 rc=$?
 tail -2 "$OUT/pytest.log"
 if [ $rc -ne 0 ]; then grep -E "FAILED|Error" "$OUT/pytest.log" | head -20; exit $rc; fi
