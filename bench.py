@@ -668,6 +668,12 @@ def main():
         phase("extras")
         try:
             rec["extras"] = run_extras(rabit, torch, dev, world)
+            lp = rec["extras"].get("link_probe_min_over_ranks")
+            if lp and lp.get("all_links_read_GBps"):
+                # a two-shot allreduce brings 2(n-1)/n of the buffer into every rank, so busbw is
+                # bounded by the rate at which one rank can read from all its peers at once
+                rec["extras"]["busbw_over_all_links_read"] = round(
+                    rec["busbw_GBps"] / lp["all_links_read_GBps"], 3)
         except Exception as e:  # noqa: BLE001
             failures.append("extras: %s: %s" % (type(e).__name__, e))
     emit_headline("; ".join(failures) if failures else None)
