@@ -670,8 +670,9 @@ def main():
             rec["extras"] = run_extras(rabit, torch, dev, world)
             lp = rec["extras"].get("link_probe_min_over_ranks")
             if lp and lp.get("all_links_read_GBps"):
-                # a two-shot allreduce brings 2(n-1)/n of the buffer into every rank, so busbw is
-                # bounded by the rate at which one rank can read from all its peers at once
+                # the pull two-shot brings 2(n-1)/n of the buffer into every rank, so its busbw is
+                # bounded by the rate at which one rank reads from all its peers at once; the push
+                # forms send half of it out instead, so with them the ratio can pass 1
                 rec["extras"]["busbw_over_all_links_read"] = round(
                     rec["busbw_GBps"] / lp["all_links_read_GBps"], 3)
         except Exception as e:  # noqa: BLE001
