@@ -288,8 +288,9 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // A second destination (the robust engine's user buffer) may only change once the op has
   // succeeded on this rank, so that a retry after a failure still finds the input there.  The
   // gather of the LAST chunk follows the op's last barrier and stores it in the same pass; the
-  // chunks before it are gathered into `out` alone and copied over after the loop, by a copy the
-  // group's failure word guards (it does nothing if any barrier of the op gave up).  The fused
+  // chunks before it are gathered into `out` alone and copied over by extra segments of that same
+  // launch, which the group's failure word guards (it does nothing if any barrier of the op gave
+  // up), so the local copy runs while the last gather reads over the links.  The fused
   // kernels hand tiles over one by one, with no last barrier: a peer dying inside one leaves some
   // tiles delivered and others not, so they never store the second destination themselves.
   const size_t last_off = count == 0 || !defer_second_ ? 0 : (count - 1) / chunk * chunk;
@@ -558,8 +559,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     XRABIT_TRY_HIP(mark(5));
   }
   if (out2 != nullptr && tail_end > 0) {
-    // the chunks before the last (and fused chunks) into the second destination, only if every
-    // barrier and hand-off of the op held
+    // fused chunks (and chunks before a fused last one) into the second destination, only if
+    // every barrier and hand-off of the op held
     CopyBatch b;
     NewBatch(&b);
     AddSeg(&b, out2, out, nullptr, tail_end * tn);
