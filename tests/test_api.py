@@ -50,6 +50,10 @@ def test_single_node_without_tracker(native_build):
         assert v == 0
         rabit.checkpoint({"a": 1})
         assert rabit.version_number() == 1
+        # no direct transport without a GPU and peers: the link probe says so instead of failing
+        assert rabit.link_probe(1 << 20) is None
+        # the direct-transport knobs report "not up" rather than raising
+        assert rabit.set_device_transport(rabit.TRANSPORT_DIRECT, "pipelined") is False
     finally:
         rabit.finalize()
 
