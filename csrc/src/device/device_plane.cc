@@ -992,12 +992,17 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
 }
 
 int DevicePlane::GraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream) {
-  if (comm_ == nullptr) return -2;
   ncclDataType_t t;
   ncclRedOp_t o;
   if (!RcclType(dtype, &t) || !RcclOp(op, &o)) return -3;
   if (count == 0) return 0;
   DeviceGuard dg(device_);
+  if (peers_ != nullptr && (comm_ == nullptr || UseDirect(count * TypeBytes(dtype)))) {
+    // the direct transport's classic form, barriers numbered on the device (replayable)
+    graph_direct_ops_ += 1;
+    return peers_->AllreduceGraphable(buf, count, dtype, op, stream) == hipSuccess ? 0 : -5;
+  }
+  if (comm_ == nullptr) return -2;
   rccl_calls_ += 1;
   ncclResult_t r = ncclAllReduce(buf, buf, count, t, o, comm_, stream);
   if (r == ncclInProgress) {

@@ -346,12 +346,16 @@ class DevicePlane {
    *        succeeds on this rank, so a retry still finds the input.
    */
   /*!
-   * \brief in-place RCCL allreduce enqueued on `stream` and nothing else: no host wait, no
-   *        event, no result log, so it may be captured into a hipGraph.  Outside fault
-   *        tolerance (non-robust engines only).  0 on success, -2 without a communicator, -3
-   *        for a dtype/op RCCL lacks (BitOR), -5 when RCCL refuses the call.
+   * \brief in-place allreduce enqueued on `stream` and nothing else: no host wait, no event,
+   *        no result log, so it may be captured into a hipGraph.  RCCL, or the direct
+   *        transport's classic form with device-numbered barriers (PeerGroup::
+   *        AllreduceGraphable) when the routing sends ops of this size there or RCCL is not up.
+   *        Outside fault tolerance (non-robust engines only).  0 on success, -2 without a
+   *        transport, -3 for a dtype/op the path lacks (BitOR), -5 when the enqueue fails.
    */
   int GraphAllreduce(void *buf, size_t count, int dtype, int op, hipStream_t stream);
+  /*! \brief graphable allreduces that went over the direct transport */
+  uint64_t graph_direct_ops() const { return graph_direct_ops_; }
   Status Allreduce(const void *send, void *recv, void *recv2, size_t count, int dtype, int op,
                    int prep, double alpha, const FailureProbe &probe);
   /*! \brief launcher of a user device reduction (IEngine::DeviceReduceLauncher) */
@@ -517,6 +521,7 @@ class DevicePlane {
   std::vector<PeerLinkInfo> links_;
   uint64_t rccl_calls_{0}, rccl_settled_{0}, rccl_aborts_{0}, init_abandoned_{0};
   uint64_t done_words_{0};
+  uint64_t graph_direct_ops_{0};
   void *warm_{nullptr};  // 4 KiB of HBM for the bring-up's connection warm-up
   int rccl_fail_streak_{0};  // aborted RCCL ops since the last op that completed
 };

@@ -228,9 +228,9 @@ hipError_t PeerGroup::Barrier(const ResolveArgs *resolve) {
   for (int p = 0; p < kMaxPeers; ++p) {
     t.p[p] = p < n_ ? reinterpret_cast<unsigned long long *>(peer_base_[p]) : nullptr;
   }
-  ++epoch_;
-  return LaunchPeerBarrier(t, rank_, n_, epoch_, &host_words_[0], dev_status(), &host_words_[1],
-                           deadline_ticks_, resolve, stream_);
+  ++epoch_;  // (statistics: the barrier's number itself lives in barrier_counter())
+  return LaunchPeerBarrier(t, rank_, n_, barrier_counter(), &host_words_[0], dev_status(),
+                           &host_words_[1], deadline_ticks_, resolve, stream_);
 }
 
 #define XRABIT_TRY_HIP(expr)              \
@@ -639,6 +639,34 @@ hipError_t PeerGroup::LinkProbe(size_t bytes, double out[kLinkProbeValues]) {
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return err;
+}
+
+hipError_t PeerGroup::AllreduceGraphable(void *buf, size_t count, int dtype, int op,
+                                         hipStream_t stream) {
+  // the classic forms only: the fused kernels and the pipelined form number their hand-offs
+  // on the host, which a replayed graph would repeat
+  const hipStream_t saved_stream = stream_;
+  const bool saved_timing = timing_, saved_fused = fused_, saved_pipe = pipeline_,
+             saved_done = done_signal_;
+  const size_t saved_fused_oneshot = fused_oneshot_max_;
+  stream_ = stream;
+  timing_ = false;
+  fused_ = false;
+  pipeline_ = false;
+  done_signal_ = false;
+  fused_oneshot_max_ = 0;
+  hipError_t e = Allreduce(buf, buf, nullptr, count, dtype, op, kPrepCopy, 1.0);
+  if (e == hipSuccess) e = Barrier();
+  stream_ = saved_stream;
+  timing_ = saved_timing;
+  fused_ = saved_fused;
+  pipeline_ = saved_pipe;
+  done_signal_ = saved_done;
+  fused_oneshot_max_ = saved_fused_oneshot;
+  done_pending_ = false;
+  timing_pending_ = false;
+  ++graphable_ops_;
+  return e;
 }
 
 void PeerGroup::DieMidOp() {

@@ -150,10 +150,16 @@ hipError_t LaunchFusedAllreduce(const FusedAllreduceArgs &args, int grid, hipStr
  *  over args.count; stage copy, per-tile ready flags, reduce of all n stages into out / out2) */
 hipError_t LaunchFusedOneshot(const FusedAllreduceArgs &args, int grid, hipStream_t stream);
 
-hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
-                             const volatile int *abort_word, int *dev_status, int *host_status,
-                             long long deadline_ticks, const ResolveArgs *resolve,
-                             hipStream_t stream);
+/*!
+ * \brief the group's flag barrier.  Its number comes from `counter`, a word in this rank's own
+ *        flag area that the barrier kernel itself advances: every rank runs the same sequence
+ *        of barriers, so the counters agree, and a captured hipGraph that replays barriers gets
+ *        fresh numbers on every replay (a host-side number would be baked into the graph)
+ */
+hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n,
+                             unsigned long long *counter, const volatile int *abort_word,
+                             int *dev_status, int *host_status, long long deadline_ticks,
+                             const ResolveArgs *resolve, hipStream_t stream);
 hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream);
 
 /*! \brief fixed-size record every rank contributes when a group is built */
@@ -260,6 +266,15 @@ class PeerGroup {
    */
   hipError_t LinkProbe(size_t bytes, double out[5]);
   static constexpr int kLinkProbeValues = 5;
+  /*!
+   * \brief in-place allreduce that may be captured into a hipGraph and replayed (non-fault-
+   *        tolerant engines): the classic pull / push form on `stream`, with no host wait, no
+   *        event and no completion word, closed by one more barrier, so no stage read of the op
+   *        outlives it and every replay may start on any stage parity.  Barrier numbers come
+   *        from the device counter.  Graph replays and other ops of the group must be ordered
+   *        (one stream, or joined streams).
+   */
+  hipError_t AllreduceGraphable(void *buf, size_t count, int dtype, int op, hipStream_t stream);
   /*! \brief make spinning barriers give up (host side; safe at any time) */
   void SignalAbort();
   /*! \brief true when a barrier gave up (read after the stream drained) */
@@ -290,6 +305,7 @@ class PeerGroup {
   /*! \brief bytes per pipeline chunk (0: ArPipeline::AutoChunk) */
   void set_pipeline_chunk(size_t bytes) { pipeline_chunk_ = bytes; }
   uint64_t pipelined_ops() const { return pipelined_ops_; }
+  uint64_t graphable_ops() const { return graphable_ops_; }
   uint64_t pipelined_rounds() const { return pipelined_rounds_; }
   /*!
    * \brief test hook (mock_die_mid): the next multi-chunk allreduce exits the process in the
@@ -373,6 +389,9 @@ class PeerGroup {
   unsigned int *done_count() const {
     return reinterpret_cast<unsigned int *>(base_ + kPeerStatusOffset + 256);
   }
+  unsigned long long *barrier_counter() const {
+    return reinterpret_cast<unsigned long long *>(base_ + kPeerStatusOffset + 512);
+  }
   unsigned long long *done_word() const {
     return reinterpret_cast<unsigned long long *>(host_words_ + 8);  // bytes 32..39
   }
@@ -410,6 +429,7 @@ class PeerGroup {
   bool pipeline_{false};
   size_t pipeline_chunk_{0};
   uint64_t pipelined_ops_{0}, pipelined_rounds_{0};
+  uint64_t graphable_ops_{0};
   bool die_mid_{false};
   bool defer_second_{true};
   bool fused_{true};

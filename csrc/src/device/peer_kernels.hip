@@ -6,7 +6,9 @@
  * Barrier: every rank owns an array of one 64-bit flag per peer inside its IPC-exported,
  * uncached staging allocation.  Arriving at barrier number e, rank r stores e into slot r of
  * every peer's array (system-scope release) and then spins until all n slots of its own array
- * are >= e (system-scope acquire).  Epochs only grow, so flags never need resetting.  Each lane
+ * are >= e (system-scope acquire).  Epochs only grow, so flags never need resetting.  The
+ * number e is kept on the device (a counter word the barrier kernel advances), so barriers
+ * recorded in a hipGraph are numbered afresh on every replay.  Each lane
  * polls with s_sleep back-off and gives up when the host raises the abort word (peer failure
  * seen on the TCP control plane) or the wall-clock deadline passes — every wave reaches an exit.
  * A failure is recorded in a device word (the guard every later kernel of the group checks
@@ -36,7 +38,7 @@ constexpr size_t kTileBytes = static_cast<size_t>(kBlock) * kUnroll * 16;
 
 template <bool RESOLVE>
 __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int rank, int n,
-                                                        unsigned long long epoch,
+                                                        unsigned long long *counter,
                                                         const volatile int *abort_word,
                                                         int *dev_status, int *host_status,
                                                         long long deadline_ticks,
@@ -44,6 +46,15 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
   const int t = threadIdx.x;
   // an earlier barrier of this group failed: stay failed, signal nothing
   if (__hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  // this barrier's number: one more than the last barrier of this rank's group (kernels of the
+  // group run one after the other on one stream, so a plain read-modify-write by one lane holds)
+  __shared__ unsigned long long s_epoch;
+  if (t == 0) {
+    s_epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __hip_atomic_store(counter, s_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const unsigned long long epoch = s_epoch;
   auto mailbox = [&](int p) {
     return reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(flags.p[p]) +
                                                   kPeerMailboxOffset) +
@@ -183,18 +194,20 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
 }
 }  // namespace
 
-hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n, unsigned long long epoch,
-                             const volatile int *abort_word, int *dev_status, int *host_status,
-                             long long deadline_ticks, const ResolveArgs *resolve,
-                             hipStream_t stream) {
-  if (n < 1 || n > kMaxPeers || rank < 0 || rank >= n) return hipErrorInvalidValue;
+hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n,
+                             unsigned long long *counter, const volatile int *abort_word,
+                             int *dev_status, int *host_status, long long deadline_ticks,
+                             const ResolveArgs *resolve, hipStream_t stream) {
+  if (n < 1 || n > kMaxPeers || rank < 0 || rank >= n || counter == nullptr) {
+    return hipErrorInvalidValue;
+  }
   if (resolve != nullptr) {
     hipLaunchKernelGGL(PeerBarrierKernel<true>, dim3(1), dim3(64), 0, stream, flags, rank, n,
-                       epoch, abort_word, dev_status, host_status, deadline_ticks, *resolve);
+                       counter, abort_word, dev_status, host_status, deadline_ticks, *resolve);
   } else {
     ResolveArgs none{};
     hipLaunchKernelGGL(PeerBarrierKernel<false>, dim3(1), dim3(64), 0, stream, flags, rank, n,
-                       epoch, abort_word, dev_status, host_status, deadline_ticks, none);
+                       counter, abort_word, dev_status, host_status, deadline_ticks, none);
   }
   return hipGetLastError();
 }

@@ -714,20 +714,21 @@ int EngineBase::DevGraphAllreduce(void *buf, size_t count, int dtype, int op,
   }
   if (GetWorldSize() == 1 && !world1_transport_) return 0;  // a one-rank reduction is identity
   device::DeviceGuard dg(dev_->device());
-  if (!dev_->has_comm()) {
+  if (!dev_->ready()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-      *why = "graph allreduce: make one eager call before capturing (it brings RCCL up)";
+      *why = "graph allreduce: make one eager call before capturing (it brings the device "
+             "transports up)";
       return -2;
     }
-    if (EnsureDeviceComm() != Status::kSuccess || !dev_->has_comm()) {
-      *why = "graph allreduce needs an RCCL communicator";
+    if (EnsureDeviceComm() != Status::kSuccess || !dev_->ready()) {
+      *why = "graph allreduce needs a device transport (RCCL or direct)";
       return -2;
     }
   }
   const int r = dev_->GraphAllreduce(buf, count, dtype, op, stream);
-  if (r == -3) *why = "graph allreduce: dtype/op not supported by RCCL";
-  if (r == -5) *why = "graph allreduce: ncclAllReduce failed";
+  if (r == -3) *why = "graph allreduce: dtype/op not supported (BitOR)";
+  if (r == -5) *why = "graph allreduce: the enqueue failed";
   if (r == 0) stats_.n_device_ops += 1;
   return r;
 }
@@ -865,6 +866,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"direct_pipeline\":" << (dev_ && dev_->pipeline() ? 1 : 0)
      << ",\"pipelined_ops\":" << (dev_ ? dev_->pipelined_ops() : 0)
      << ",\"pipelined_rounds\":" << (dev_ ? dev_->pipelined_rounds() : 0)
+     << ",\"graph_direct_ops\":" << (dev_ ? dev_->graph_direct_ops() : 0)
      << ",\"direct_fused\":" << (dev_ && dev_->fused() ? 1 : 0)
      << ",\"calib_heap_src\":" << (calib_heap_src_ ? 1 : 0)
      << ",\"rccl_init_failed\":" << rccl_failed_

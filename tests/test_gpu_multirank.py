@@ -103,6 +103,18 @@ def test_link_probe(world):
     assert out.count("LINKPROBE OK") == world, out[-3000:]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_graphable_allreduce_direct_multirank(world):
+    """allreduce_graphable over the direct transport captured into hipGraphs and replayed with
+    several ranks: device-numbered barriers resynchronise every replay, eager ops in between
+    stay exact, and a graphed data-parallel step reduces world x the local gradient"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("graph_direct.py", world)
+    assert rc == 0, out[-5000:]
+    assert out.count("GRAPHDIRECT OK") == world, out[-3000:]
+
+
 def test_result_log_spills_to_host():
     """an HBM result log capped below one iteration's results: the entries past the cap live in
     pinned host memory, and killed ranks replay both kinds (HBM and spilled) from survivors"""
