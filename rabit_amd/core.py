@@ -473,11 +473,15 @@ def link_probe(nbytes: int = 64 << 20) -> Optional[dict]:
 
 
 def allreduce_graphable(t, op: int):
-    """In-place RCCL allreduce of an HBM tensor on the current stream, with no host-side
+    """In-place allreduce of an HBM tensor on the current stream, with no host-side
     synchronisation: unlike allreduce(), it can be captured into a hipGraph with the rest of
-    the step (torch.cuda.graph / rabit_amd.parallel.GraphedStep).  Non-fault-tolerant engines
-    only (init(lib="base")): the op has no sequence number, result log or replay.  Identity at
-    world size 1 without a communicator."""
+    the step (torch.cuda.graph / rabit_amd.parallel.GraphedStep).  It runs over RCCL, or over
+    the direct transport (classic form, barriers numbered on the device so every replay
+    resynchronises) when the routing sends this size there or RCCL is not up.  Graph replays
+    and other collectives must be ordered on the GPU (one stream, or joined streams).  Make one
+    eager call before capturing (it brings the transports up).  Non-fault-tolerant engines only
+    (init(lib="base")): the op has no sequence number, result log or replay.  Identity at world
+    size 1 without a device transport."""
     import torch
 
     _check_init()

@@ -95,13 +95,14 @@ class GradientBuckets:
         """Allreduce every bucket (in place); returns the buckets.
 
         graphable=True: HBM buckets go through `rabit.allreduce_graphable` (a bare in-place
-        ncclAllReduce on the current stream, no host synchronisation), so the call can sit
-        inside a captured hipGraph with the rest of the step.  Non-fault-tolerant engines only
-        (init(lib="base")); averaging is one `mul_` on the same stream, captured as well.
-        Limits: a replayed graph has no deadline and no failure probe (a dead peer hangs
-        replay(); this is the base engine's contract), and multi-rank capture has only run with
-        a one-rank communicator so far (tests/scripts/graph_allreduce.py checks the reduced
-        values against world x the local gradient, so the first multi-GPU run verifies it)."""
+        allreduce on the current stream over RCCL or the direct transport, no host
+        synchronisation), so the call can sit inside a captured hipGraph with the rest of the
+        step.  Non-fault-tolerant engines only (init(lib="base")); averaging is one `mul_` on the
+        same stream, captured as well.  Limits: a replayed graph has no failure probe (a dead
+        peer stalls replay() until the direct barriers' deadline, or hangs RCCL; this is the base
+        engine's contract).  Multi-rank capture over the direct transport is tested
+        (tests/scripts/graph_direct.py: replayed buckets equal world x the local gradient); a
+        captured multi-rank RCCL reduction has only run with a one-rank communicator so far."""
         world = rabit.get_world_size()
         if graphable:
             for b in self.buckets:
