@@ -655,7 +655,12 @@ hipError_t PeerGroup::AllreduceGraphable(void *buf, size_t count, int dtype, int
   pipeline_ = false;
   done_signal_ = false;
   fused_oneshot_max_ = 0;
-  hipError_t e = Allreduce(buf, buf, nullptr, count, dtype, op, kPrepCopy, 1.0);
+  // A replay runs its stage parities as captured, whatever the op before it left behind: a
+  // barrier on each side keeps every peer's reads of the neighbouring ops out of this op's
+  // stage writes (the previous op has completed on every rank once all arrive here; nobody
+  // starts the next op before all finished this one).
+  hipError_t e = Barrier();
+  if (e == hipSuccess) e = Allreduce(buf, buf, nullptr, count, dtype, op, kPrepCopy, 1.0);
   if (e == hipSuccess) e = Barrier();
   stream_ = saved_stream;
   timing_ = saved_timing;

@@ -269,8 +269,9 @@ class PeerGroup {
   /*!
    * \brief in-place allreduce that may be captured into a hipGraph and replayed (non-fault-
    *        tolerant engines): the classic pull / push form on `stream`, with no host wait, no
-   *        event and no completion word, closed by one more barrier, so no stage read of the op
-   *        outlives it and every replay may start on any stage parity.  Barrier numbers come
+   *        event and no completion word, between two extra barriers, so no stage access of the
+   *        op overlaps one of the ops around it and a replay may run on any stage parity (its
+   *        parities are the captured ones, whatever the previous op used).  Barrier numbers come
    *        from the device counter.  Graph replays and other ops of the group must be ordered
    *        (one stream, or joined streams).
    */
