@@ -5,6 +5,7 @@ ops captured into one hipGraph (allreduce_graphable) and replayed.  Ranks share 
     python -m rabit_amd.launcher -n 2 -- python tools/graph_direct_bench.py
 """
 import json
+import os
 import sys
 import time
 
@@ -19,7 +20,10 @@ def main():
     rank, world = rabit.get_rank(), rabit.get_world_size()
     dev = torch.device("cuda", 0)
     side = torch.cuda.Stream()
-    for nbytes in (4096, 1 << 20, 16 << 20):
+    sizes = (4096, 1 << 20, 16 << 20)
+    if os.environ.get("XR_SIZES"):
+        sizes = tuple(int(v) for v in os.environ["XR_SIZES"].split(","))
+    for nbytes in sizes:
         x = torch.full((nbytes // 4,), float(rank + 1), device=dev)
         ops = 64 if nbytes <= (1 << 20) else 16
         # eager (host waits for each op)
