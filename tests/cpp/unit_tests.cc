@@ -988,8 +988,10 @@ TEST(link_reset_discards_stale_bytes) {
   EXPECT(b.SendAll(junk_b.data(), junk_b.size()) == junk_b.size());
   std::vector<rabit::net::TcpSocket *> la = {&a}, lb = {&b};
   rabit::net::Status ra = rabit::net::Status::kSockError, rb = ra;
-  std::thread t([&]() { rb = rabit::net::ResetLinks(lb, 5000); });
-  ra = rabit::net::ResetLinks(la, 5000);
+  // a generous deadline: under ThreadSanitizer on a loaded machine a side can be descheduled for
+  // seconds (a passing run takes milliseconds)
+  std::thread t([&]() { rb = rabit::net::ResetLinks(lb, 20000); });
+  ra = rabit::net::ResetLinks(la, 20000);
   t.join();
   EXPECT(ra == rabit::net::Status::kSuccess && rb == rabit::net::Status::kSuccess);
   a.SetNonBlock(false);
