@@ -212,8 +212,13 @@ def run_extras(rabit, torch, dev, world):
         # xGMI per-link and all-link bandwidth, reads / writes / both ways (direct transport's
         # IPC mappings; on ranks sharing one GPU this is HBM): min over ranks
         phase("link probe")
-        lp = rabit.link_probe(64 << 20)
-        if lp is not None:
+        try:
+            lp = rabit.link_probe(64 << 20)
+        except RuntimeError as e:  # a failed probe costs its own numbers, not the other extras
+            lp = None
+            out["link_probe_error"] = str(e)
+        ok = rabit.allreduce(np.array([0 if lp is None else 1], dtype=np.int32), rabit.MIN)[0]
+        if ok:
             keys = sorted(lp)
             low = rabit.allreduce(np.array([lp[k] for k in keys]), rabit.MIN)
             out["link_probe_min_over_ranks"] = {k: round(float(v), 2) for k, v in zip(keys, low)}
