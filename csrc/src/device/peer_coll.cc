@@ -685,12 +685,13 @@ void PeerGroup::DieMidOp() {
 
 hipError_t PeerGroup::AllreducePipelined(const char *in, char *out, char *out2, size_t count,
                                          size_t tn, double post, const ReduceStep &step) {
-  const size_t chunk =
-      pipeline_chunk_ != 0
-          ? std::max<size_t>(256 * static_cast<size_t>(n_),
-                             pipeline_chunk_ / tn / (256 * static_cast<size_t>(n_)) *
-                                 (256 * static_cast<size_t>(n_)))
-          : ArPipeline::AutoChunk(count, tn, n_, stage_bytes_);
+  // a configured chunk is rounded to whole 256 n-element blocks and held to what n + 1 slots
+  // of a stage can take (the automatic choice already is)
+  const size_t q = 256 * static_cast<size_t>(n_);
+  const size_t cap = stage_bytes_ / tn / static_cast<size_t>(n_ + 1) / 256 * q;
+  const size_t chunk = pipeline_chunk_ != 0
+                           ? std::max(q, std::min(cap, pipeline_chunk_ / tn / q * q))
+                           : ArPipeline::AutoChunk(count, tn, n_, stage_bytes_);
   const ArPipeline plan(count, chunk, n_);
   utils::Check(plan.stage_bytes(tn) <= stage_bytes_,
                "pipelined allreduce: a chunk of %zu elements needs %zu stage bytes, %zu available",
