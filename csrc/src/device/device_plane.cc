@@ -175,6 +175,8 @@ int DevicePlane::DeviceCount() {
   return n;
 }
 
+void DevicePlane::ConfigureRcclEnv() { setenv("NCCL_RUNTIME_CONNECT", "0", 0); }
+
 DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   const int ndev = DeviceCount();
   utils::Check(ndev > 0, "DevicePlane: no HIP device visible");
@@ -185,10 +187,6 @@ DevicePlane::DevicePlane(const DeviceConfig &cfg, int rank_hint) : cfg_(cfg) {
   }
   device_ = dev % ndev;
   CheckHip(hipSetDevice(device_), "hipSetDevice");
-  // connect RCCL's collective channels at communicator init (InitComm's helper thread, watched
-  // by the failure probe) instead of lazily inside the first collective that needs them, where
-  // a dead peer would block the enqueueing thread with no deadline.  A user setting wins.
-  setenv("NCCL_RUNTIME_CONNECT", "0", 0);
   CheckHip(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking), "hipStreamCreate");
   CheckHip(hipEventCreateWithFlags(&ev_switch_, hipEventDisableTiming), "hipEventCreate");
   stream_ = cfg_.ops_on_user_stream ? user_stream_ : own_stream_;
@@ -231,7 +229,6 @@ DevicePlane::~DevicePlane() {
     if (scratch_[i] != nullptr) (void)hipFree(scratch_[i]);
   }
   if (pinned_ != nullptr) (void)hipHostFree(pinned_);
-  if (warm_ != nullptr) (void)hipFree(warm_);
   if (ev_in_ != nullptr) (void)hipEventDestroy(ev_in_);
   if (ev_done_ != nullptr) (void)hipEventDestroy(ev_done_);
   peers_.reset();
@@ -263,6 +260,9 @@ namespace {
  *        thread that runs it.  The helper may outlive the waiter's interest (a peer died inside
  *        RCCL's bootstrap, which waits on sockets without any deadline): the waiter then
  *        abandons it, and a helper that ever returns aborts the communicator it built itself.
+ *        The warm-up stream and buffer belong to this state, not to the plane: an abandoned
+ *        helper that wakes up later enqueues nothing on a stream the plane reuses or frees, and
+ *        whoever drops the state last releases them (once idle).
  */
 struct CommBringUp {
   std::mutex mu;
@@ -270,13 +270,41 @@ struct CommBringUp {
   bool done{false}, abandoned{false};
   ncclResult_t result{ncclSuccess};
   ncclComm_t comm{nullptr};
+  hipStream_t stream{nullptr};
+  char *buf{nullptr};
+  size_t buf_bytes{0};
+  ~CommBringUp() {
+    // work still queued (an aborted warm-up that never drained): leak rather than free memory
+    // a kernel may still touch
+    const bool idle = stream == nullptr || hipStreamQuery(stream) == hipSuccess;
+    (void)hipGetLastError();
+    if (!idle) return;
+    if (buf != nullptr) (void)hipFree(buf);
+    if (stream != nullptr) (void)hipStreamDestroy(stream);
+  }
 };
+/*! \brief helpers abandoned in RCCL's bootstrap that have not returned yet (process-wide) */
+std::atomic<int> g_live_abandoned{0};
 }  // namespace
+
+int DevicePlane::LiveAbandonedInits() { return g_live_abandoned.load(); }
 
 Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
                              const FailureProbe &probe) {
   if (comm_ != nullptr) AbortComm();
   utils::Check(id_bytes.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size");
+  if (nranks > 1 && g_live_abandoned.load() >= kMaxAbandonedInits) {
+    // every abandoned helper holds a thread and RCCL's bootstrap sockets until its peer shows
+    // up, which it may never do: beyond the cap no new multi-rank bring-up starts.  The engine
+    // then runs on the direct transport, or fails for a restart when none is left.
+    rccl_fail_streak_ += 1;
+    utils::Check(cfg_.rccl_max_failures <= 0 || rccl_fail_streak_ <= cfg_.rccl_max_failures,
+                 "RCCL bring-up failed %d times in a row; giving up", rccl_fail_streak_);
+    utils::HandleLogInfo("[xrabit] RCCL bring-up refused: %d abandoned bring-ups still blocked "
+                         "in RCCL's bootstrap\n", g_live_abandoned.load());
+    init_refused_ += 1;
+    return Status::kAborted;
+  }
   ncclUniqueId id;
   std::memcpy(id.internal, id_bytes.data(), sizeof(id.internal));
   CheckHip(hipSetDevice(device_), "hipSetDevice");
@@ -290,33 +318,42 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
   // not help here: ncclCommInitRankConfig with blocking = 0 still blocks the caller inside the
   // bootstrap while a rank is missing (measured: profiles/r3_rccl_lifecycle/).  The helper runs
   // the init and then connects every channel this job will use (eager collective connections,
-  // NCCL_RUNTIME_CONNECT=0, set by the constructor; plus one grouped send/recv with every peer
-  // and a one-element allreduce), all while the ranks are known to be alive.  Afterwards no
-  // RCCL call of this epoch waits on a peer on the host: only kernels do, and WaitEvent aborts
-  // those.  This thread meanwhile watches the failure probe and the deadline.
+  // NCCL_RUNTIME_CONNECT=0, set by the engine at start-up; plus one grouped send/recv with every
+  // peer and one allreduce per size class the routing may send to RCCL), all while the ranks
+  // are known to be alive.  Afterwards no RCCL call of this epoch waits on a peer on the host:
+  // only kernels do, and WaitEvent aborts those.  This thread meanwhile watches the failure
+  // probe and the deadline.
   config.blocking = 1;
-  if (warm_ == nullptr) CheckHip(hipMalloc(&warm_, 4096), "hipMalloc(rccl warm-up)");
   auto g = std::make_shared<CommBringUp>();
+  CheckHip(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking), "hipStreamCreate(warm-up)");
+  // size classes of the warm-up: 64 KiB (latency algorithms), 4 MiB (gradient buckets) and the
+  // large point (128 MiB by default): each reaches the protocol RCCL picks for that size
+  const size_t big = std::max<size_t>(cfg_.rccl_warm_bytes, 4096) / 256 * 256;
+  g->buf_bytes = nranks > 1 ? big : 4096;
+  if (hipMalloc(&g->buf, g->buf_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    g->buf_bytes = 4096;
+    CheckHip(hipMalloc(&g->buf, g->buf_bytes), "hipMalloc(rccl warm-up)");
+  }
   const int dev = device_;
-  hipStream_t ws = own_stream_;
-  char *wbuf = static_cast<char *>(warm_);
-  std::thread([g, id, nranks, rank, config, dev, ws, wbuf]() mutable {
+  std::thread([g, id, nranks, rank, config, dev]() mutable {
     (void)hipSetDevice(dev);
     ncclComm_t c = nullptr;
     ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &config);
     {
-      // given up on while the init blocked: the plane (its warm-up stream and buffer) may be
-      // gone already, so touch nothing of it
       std::lock_guard<std::mutex> lk(g->mu);
       if (g->abandoned) {
         g->done = true;
         if (c != nullptr) ncclCommAbort(c);
+        g_live_abandoned.fetch_sub(1);
         return;
       }
     }
+    hipStream_t ws = g->stream;
+    char *wbuf = g->buf;
     if (r == ncclSuccess && nranks > 1) {
       // every p2p pair (RCCL connects send/recv channels lazily inside ncclGroupEnd) and the
-      // allreduce path, with 1-byte / 1-element payloads
+      // allreduce paths, 1-byte p2p payloads
       r = ncclGroupStart();
       for (int p = 0; p < nranks && r == ncclSuccess; ++p) {
         if (p == rank) continue;
@@ -325,8 +362,13 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
       }
       const ncclResult_t e = ncclGroupEnd();
       if (r == ncclSuccess) r = e;
-      if (r == ncclSuccess) {
-        r = ncclAllReduce(wbuf + 4088, wbuf + 4088, 1, ncclFloat32, ncclSum, c, ws);
+      const size_t classes[3] = {64u << 10, 4u << 20, g->buf_bytes};
+      size_t last = 0;
+      for (size_t bytes : classes) {
+        bytes = std::min(bytes, g->buf_bytes);
+        if (r != ncclSuccess || bytes <= last) continue;
+        last = bytes;
+        r = ncclAllReduce(wbuf, wbuf, bytes / 4, ncclFloat32, ncclSum, c, ws);
       }
     }
     bool abandoned;
@@ -338,7 +380,10 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
       abandoned = g->abandoned;
     }
     g->cv.notify_all();
-    if (abandoned && c != nullptr) ncclCommAbort(c);  // nobody else will ever use it
+    if (abandoned) {
+      if (c != nullptr) ncclCommAbort(c);  // nobody else will ever use it
+      g_live_abandoned.fetch_sub(1);
+    }
   }).detach();
   core::WaitScope waiting;  // the bootstrap waits on every peer
   using clock = std::chrono::steady_clock;
@@ -373,26 +418,40 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
         break;
       }
     }
-    if (!done) g->abandoned = true;  // the helper aborts what it built, if it ever returns
+    if (!done) {
+      g->abandoned = true;  // the helper aborts what it built, if it ever returns
+      g_live_abandoned.fetch_add(1);
+    }
   }
   if (!done) {
     rccl_aborts_ += 1;
     init_abandoned_ += 1;
+    // an abandoned bring-up counts like an aborted op: a job whose communicators never come up
+    // stops after rccl_max_failures of them instead of leaking helpers forever
+    rccl_fail_streak_ += 1;
     utils::HandleLogInfo("[xrabit] RCCL communicator bring-up %s after %.1f s: abandoned (the "
-                         "helper thread stays blocked in RCCL's bootstrap)\n",
+                         "helper thread stays blocked in RCCL's bootstrap; %d live)\n",
                          fail == Status::kTimeout ? "timed out" : "lost a peer",
-                         std::chrono::duration<double>(clock::now() - t0).count());
+                         std::chrono::duration<double>(clock::now() - t0).count(),
+                         g_live_abandoned.load());
+    utils::Check(cfg_.rccl_max_failures <= 0 || rccl_fail_streak_ <= cfg_.rccl_max_failures,
+                 "RCCL bring-up failed %d times in a row; giving up", rccl_fail_streak_);
     return fail;
   }
   comm_ = g->comm;
   if (g->result != ncclSuccess) {
     utils::HandleLogInfo("[xrabit] RCCL communicator bring-up failed: %s\n",
                          ncclGetErrorString(g->result));
+    rccl_fail_streak_ += 1;
     if (comm_ != nullptr) {
       rccl_aborts_ += 1;
-      AbortComm();  // drains the warm-up kernels the helper may have enqueued
+      AbortComm();
     }
     comm_ = nullptr;
+    // the warm-up kernels were aborted with the communicator: let them leave the stream
+    DrainBringUp(g->stream);
+    utils::Check(cfg_.rccl_max_failures <= 0 || rccl_fail_streak_ <= cfg_.rccl_max_failures,
+                 "RCCL bring-up failed %d times in a row; giving up", rccl_fail_streak_);
     return Status::kAborted;
   }
   nranks_ = nranks;
@@ -402,13 +461,26 @@ Status DevicePlane::InitComm(const std::string &id_bytes, int nranks, int rank,
     // deadline, abort on failure)
     hipEvent_t ev = nullptr;
     CheckHip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(warm-up)");
-    CheckHip(hipEventRecord(ev, own_stream_), "hipEventRecord(warm-up)");
-    op_bytes_ = 0;
+    CheckHip(hipEventRecord(ev, g->stream), "hipEventRecord(warm-up)");
+    op_bytes_ = g->buf_bytes;
     const Status s = WaitEvent(ev, probe);
     (void)hipEventDestroy(ev);
-    if (s != Status::kSuccess) return s;  // WaitEvent aborted the communicator
+    if (s != Status::kSuccess) {
+      DrainBringUp(g->stream);
+      return s;  // WaitEvent aborted the communicator
+    }
   }
   return Status::kSuccess;
+}
+
+void DevicePlane::DrainBringUp(hipStream_t s) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  while (hipStreamQuery(s) == hipErrorNotReady &&
+         std::chrono::duration<double>(clock::now() - t0).count() < cfg_.drain_timeout_sec) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  (void)hipGetLastError();
 }
 
 bool DevicePlane::MockRcclFault() {
@@ -662,6 +734,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_pipeline(cfg_.pipeline_mode == 1);
     peers_->set_pipeline_chunk(cfg_.pipeline_chunk);
     peers_->set_defer_second(cfg_.defer_second);
+    peers_->set_zero_copy_min(cfg_.zero_copy_min);
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();
@@ -681,6 +754,16 @@ bool DevicePlane::OpenPeers(const std::vector<PeerRecord> &all, int rank, std::s
     return false;
   }
   return true;
+}
+
+std::string DevicePlane::RegistryJson() const {
+  if (peers_ == nullptr) return "{}";
+  const PeerRegistry &r = peers_->registry();
+  return "{\"exports\":" + std::to_string(r.exports()) + ",\"imports\":" +
+         std::to_string(r.imports()) + ",\"pending\":" + std::to_string(r.pending()) +
+         ",\"unexportable\":" + std::to_string(r.unexportable()) + ",\"zero_copy_chunks\":" +
+         std::to_string(peers_->reg_zero_copy_chunks()) + ",\"opened\":" +
+         (r.opened() ? "true" : "false") + "}";
 }
 
 bool DevicePlane::DirectPhaseUs(double out[PeerGroup::kPhases], uint64_t *nops) const {

@@ -73,6 +73,9 @@ struct DeviceConfig {
                                        // 0 never, 1 always (with push), 2 as the calibration
                                        // finds faster
   size_t pipeline_chunk{0};            // its chunk in bytes (0: ArPipeline::AutoChunk)
+  size_t zero_copy_min{1u << 20};      // direct pull two-shot: ordinary HBM inputs of at least
+                                       // this size are IPC-registered and read in place by the
+                                       // peers (peer_registry.h); 0: never
   bool defer_second{true};             // multi-chunk ops: the second destination only after
                                        // the last barrier (0: test knob, the old behaviour)
   // host-buffer allreduce staged through HBM (rabit_host_via_device): pipelined in chunks of
@@ -90,6 +93,8 @@ struct DeviceConfig {
   bool done_word{true};                // small direct ops: poll a kernel-written host word for
                                        // completion instead of an event
   int rccl_max_failures{8};            // consecutive aborted RCCL ops before the error is fatal
+  size_t rccl_warm_bytes{128u << 20};  // largest allreduce of the bring-up's warm-up (64 KiB,
+                                       // 4 MiB and this size connect RCCL's algorithm paths)
   int mock_rccl_error{0};              // test hook: the n-th RCCL enqueue (1-based) fails with
                                        // ncclRemoteError instead of running
 };
@@ -162,6 +167,16 @@ class DeviceGuard {
 
 class DevicePlane {
  public:
+  /*!
+   * \brief process-wide RCCL settings the plane relies on, applied before any thread starts
+   *        (setenv is not safe against concurrent getenv): NCCL_RUNTIME_CONNECT=0 makes RCCL
+   *        connect its collective channels inside communicator init (InitComm's helper thread,
+   *        watched by the failure probe) instead of lazily inside the first collective that needs
+   *        them, where a dead peer would block the enqueueing thread with no deadline.  This is a
+   *        side effect on every RCCL user of the process (torch.distributed included): their
+   *        communicators connect eagerly too.  A value the user set wins.
+   */
+  static void ConfigureRcclEnv();
   /*! \brief number of visible GPUs (0 when HIP has no device) */
   static int DeviceCount();
   DevicePlane(const DeviceConfig &cfg, int rank_hint);
@@ -316,6 +331,13 @@ class DevicePlane {
   const SymHeapInfo &sym_heap() const { return heap_; }
   size_t sym_heap_used() const { return heap_used_; }
   uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
+  uint64_t reg_zero_copy_chunks() const { return peers_ ? peers_->reg_zero_copy_chunks() : 0; }
+  /*! \brief zero-copy registry counters as JSON ({} without a peer group) */
+  std::string RegistryJson() const;
+  /*! \brief every rank opened the group: drop the names of the shared registry pages */
+  void SealPeers() {
+    if (peers_ != nullptr) peers_->SealRegistry();
+  }
   uint64_t oneshot_ops() const { return peers_ ? peers_->oneshot_ops() : 0; }
   uint64_t fused_chunks() const { return peers_ ? peers_->fused_chunks() : 0; }
   uint64_t fused_oneshots() const { return peers_ ? peers_->fused_oneshots() : 0; }
@@ -445,11 +467,19 @@ class DevicePlane {
   uint64_t rccl_aborts() const { return rccl_aborts_; }
   /*! \brief communicator bring-ups given up while RCCL's bootstrap still waited on a peer */
   uint64_t init_abandoned() const { return init_abandoned_; }
+  /*! \brief multi-rank bring-ups refused because kMaxAbandonedInits helpers were still live */
+  uint64_t init_refused() const { return init_refused_; }
+  /*! \brief abandoned bring-up helpers of this process still blocked in RCCL */
+  static int LiveAbandonedInits();
+  /*! \brief at most this many abandoned bring-up helpers may be live at once */
+  static constexpr int kMaxAbandonedInits = 2;
   /*! \brief ops whose completion was read from a kernel-written host word */
   uint64_t done_words() const { return done_words_; }
 
  private:
   Status WaitEvent(hipEvent_t ev, const FailureProbe &probe);
+  /*! \brief wait (bounded by drain_timeout_sec) for a bring-up's warm-up stream to go idle */
+  void DrainBringUp(hipStream_t s);
   /*! \brief wait until a kernel stored `epoch` (or more) into the pinned host word */
   Status WaitWord(const volatile unsigned long long *word, unsigned long long epoch,
                   const FailureProbe &probe);
@@ -522,7 +552,7 @@ class DevicePlane {
   uint64_t rccl_calls_{0}, rccl_settled_{0}, rccl_aborts_{0}, init_abandoned_{0};
   uint64_t done_words_{0};
   uint64_t graph_direct_ops_{0};
-  void *warm_{nullptr};  // 4 KiB of HBM for the bring-up's connection warm-up
+  uint64_t init_refused_{0};
   int rccl_fail_streak_{0};  // aborted RCCL ops since the last op that completed
 };
 

@@ -101,6 +101,11 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
   local_.heap_bytes = heap_.base != nullptr ? heap_.bytes : 0;
   local_.fused_cap = FusedResidentBlocks(device_);
   std::memcpy(local_.heap_ipc, heap_.ipc, sizeof(local_.heap_ipc));
+  // zero-copy registry page (a failure only leaves ordinary inputs staged)
+  std::string rwhy;
+  if (registry_.Create(&rwhy)) {
+    std::strncpy(local_.reg_name, registry_.name(), sizeof(local_.reg_name) - 1);
+  }
   void *tbl = nullptr;
   CheckHip(hipMalloc(&tbl, kMaxPeers * sizeof(void *)), "hipMalloc(source table)");
   table_ = static_cast<const void **>(tbl);
@@ -187,6 +192,16 @@ bool PeerGroup::Open(const std::vector<PeerRecord> &all, int rank, std::string *
   }
   n_ = n;
   rank_ = rank;
+  {
+    std::vector<std::string> names(n);
+    bool all_named = true;
+    for (int r = 0; r < n; ++r) {
+      names[r] = std::string(all[r].reg_name, strnlen(all[r].reg_name, sizeof(all[r].reg_name)));
+      all_named = all_named && !names[r].empty();
+    }
+    std::string rwhy;
+    registry_ok_ = all_named && n >= 2 && registry_.Open(names, rank, &rwhy);
+  }
   // a fused launch waits on the other ranks' launches: when ranks share a GPU, no rank's grid
   // may take every slot of it, or the others' workgroups could never start; each gets at most
   // its share of the resident capacity.  Every rank derives the same grid from the same records
@@ -279,6 +294,18 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   auto mark = [&](int k) { return timed ? hipEventRecord(ev_[k], stream_) : hipSuccess; };
   bool did_fused = false;
   done_pending_ = false;
+  // Registered zero copy (peer_registry.h): every rank counts this op alike, maps the peers'
+  // newly exported allocations ahead of its kernels, and reads in place from the peers that
+  // published one.  Only the pull two-shot stages its input (push and pipelined forms read it
+  // where it is), so only that form asks for its own input to be exported.
+  ++op_seq_;
+  const bool registry = registry_ok_ && !no_registry_ && indirect;
+  if (registry) XRABIT_TRY_HIP(registry_.Refresh(op_seq_, stream_));
+  unsigned long long reg_mailbox = 0;
+  const bool reg_input = registry && zero_copy_min_ != 0 && count * tn >= zero_copy_min_ &&
+                         count * tn > oneshot_max_ && !push_ && !fused_ &&
+                         stage_prep == kPrepCopy && !InHeap(in, count * tn) &&
+                         registry_.Resolve(in, count * tn, op_seq_, &reg_mailbox);
   // pipelined push form (ar_plan.h): ops above the one-shot size, raw inputs
   if (pipeline_ && push_ && n_ >= 2 && stage_prep == kPrepCopy &&
       !(indirect && count * tn <= oneshot_max_)) {
@@ -314,9 +341,16 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     // holds: chunk is a multiple of 256 n)
     const bool use_push = push_ && !oneshot && stage_prep == kPrepCopy &&
                           n_ * seg * tn <= stage_bytes_;
-    const bool zero_copy = indirect && !oneshot && !use_push && stage_prep == kPrepCopy &&
-                           InHeap(chunk_src, c * tn) &&
-                           (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
+    const bool aligned_src = (reinterpret_cast<uintptr_t>(chunk_src) & 15u) == 0;
+    const bool heap_zero_copy = indirect && !oneshot && !use_push && stage_prep == kPrepCopy &&
+                                InHeap(chunk_src, c * tn) && aligned_src;
+    const bool reg_zero_copy = reg_input && !oneshot && !use_push && aligned_src;
+    const bool zero_copy = heap_zero_copy || reg_zero_copy;
+    // where this rank's input of the chunk is: its stage, the heap, or a registered allocation
+    const unsigned long long my_mailbox =
+        heap_zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(chunk_src - heap_.base))
+        : reg_zero_copy ? reg_mailbox + static_cast<unsigned long long>(off * tn)
+                        : static_cast<unsigned long long>(mine - base_);
     char *chunk_out = out + off * tn;
     char *chunk_out2 = out2_now != nullptr ? out2_now + off * tn : nullptr;
     // every input of this decision is the same on all ranks (the kernel copes with this rank's
@@ -344,9 +378,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.n = n_;
       fa.rank = rank_;
       fa.push = use_push ? 1 : 0;
-      fa.zero_copy = zero_copy ? 1 : 0;
-      fa.mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(chunk_src - heap_.base))
-                             : static_cast<unsigned long long>(mine - base_);
+      fa.zero_copy = heap_zero_copy ? 1 : 0;  // (reg_input is off with the fused form)
+      fa.mailbox = my_mailbox;
       fa.epoch = ++fused_epoch_;
       fa.dtype = dtype;
       fa.op = builtin_op;
@@ -419,6 +452,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       // no staging: this rank's own stage is its inbox, written by the peers
     } else if (zero_copy) {
       ++zero_copy_chunks_;
+      if (reg_zero_copy) ++reg_zero_copy_chunks_;
     } else if (stage_prep == kPrepCopy) {
       XRABIT_TRY_HIP(LaunchCopy(mine, chunk_src, c * tn, stream_));
     } else {
@@ -431,9 +465,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       // peers' inputs itself, in rank order (identical results everywhere), straight into the
       // destination — no second barrier, no gather
       ResolveArgs ra{};
-      ra.my_mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(
-                                                      chunk_src - heap_.base))
-                                : static_cast<unsigned long long>(mine - base_);
+      ra.my_mailbox = my_mailbox;
+      ra.reg_table = registry_ok_ ? registry_.device_table() : nullptr;
       ra.parity = which;
       for (int p = 0; p < n_; ++p) {
         ra.stage_base[p] = peer_base_[p];
@@ -515,9 +548,8 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     }
     if (indirect) {
       ResolveArgs ra{};
-      ra.my_mailbox = zero_copy ? (kMailboxHeap | static_cast<unsigned long long>(
-                                                      chunk_src - heap_.base))
-                                : static_cast<unsigned long long>(mine - base_);
+      ra.my_mailbox = my_mailbox;
+      ra.reg_table = registry_ok_ ? registry_.device_table() : nullptr;
       ra.parity = which;
       for (int p = 0; p < n_; ++p) {
         ra.stage_base[p] = peer_base_[p];
@@ -655,6 +687,7 @@ hipError_t PeerGroup::AllreduceGraphable(void *buf, size_t count, int dtype, int
   pipeline_ = false;
   done_signal_ = false;
   fused_oneshot_max_ = 0;
+  no_registry_ = true;  // no host drain or table copy may be captured
   // A replay runs its stage parities as captured, whatever the op before it left behind: a
   // barrier on each side keeps every peer's reads of the neighbouring ops out of this op's
   // stage writes (the previous op has completed on every rank once all arrive here; nobody
@@ -668,6 +701,7 @@ hipError_t PeerGroup::AllreduceGraphable(void *buf, size_t count, int dtype, int
   pipeline_ = saved_pipe;
   done_signal_ = saved_done;
   fused_oneshot_max_ = saved_fused_oneshot;
+  no_registry_ = false;
   done_pending_ = false;
   timing_pending_ = false;
   ++graphable_ops_;

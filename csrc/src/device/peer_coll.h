@@ -39,6 +39,8 @@
 #include <string>
 #include <vector>
 
+#include "device/peer_registry.h"
+
 namespace rabit {
 namespace device {
 
@@ -90,6 +92,8 @@ struct ResolveArgs {
   const char *heap_base[kMaxPeers];  // nullptr: that peer has no symmetric heap
   size_t seg_off;                   // byte offset of this rank's segment in the chunk
   const void **table;               // out: n source pointers
+  // registered allocations (peer_registry.h): [peer][slot] mapped bases, for kMailboxReg words
+  const char *const *reg_table;
 };
 
 /*!
@@ -174,6 +178,7 @@ struct PeerRecord {
   uint64_t heap_bytes;
   int32_t fused_cap;   // fused-kernel workgroups resident at once on this GPU
   int32_t pad;
+  char reg_name[48];   // shm name of the zero-copy registry page ("" : none, peer_registry.h)
 };
 
 /*!
@@ -281,8 +286,17 @@ class PeerGroup {
   /*! \brief true when a barrier gave up (read after the stream drained) */
   bool failed() const;
   uint64_t barriers() const { return epoch_; }
-  /*! \brief chunks whose input was read in place from the symmetric heap (no stage copy) */
+  /*! \brief chunks whose input was read in place (symmetric heap or a registered allocation:
+   *  no stage copy) */
   uint64_t zero_copy_chunks() const { return zero_copy_chunks_; }
+  /*! \brief of those, chunks of registered ordinary allocations (peer_registry.h) */
+  uint64_t reg_zero_copy_chunks() const { return reg_zero_copy_chunks_; }
+  const PeerRegistry &registry() const { return registry_; }
+  /*! \brief ordinary allocations are registered for zero copy (rabit_device_zero_copy) from
+   *  this many bytes per op (0: never) */
+  void set_zero_copy_min(size_t b) { zero_copy_min_ = b; }
+  /*! \brief every peer mapped this rank's registry page: drop its name */
+  void SealRegistry() { registry_.Seal(); }
   /*! \brief ops of at most this many bytes use the one-shot allreduce (one barrier) */
   void set_oneshot_max(size_t b) { oneshot_max_ = b; }
   /*!
@@ -423,6 +437,12 @@ class PeerGroup {
   double phase_ms_[kPhases]{};
   uint64_t timed_ops_{0};
   uint64_t zero_copy_chunks_{0};
+  uint64_t reg_zero_copy_chunks_{0};
+  PeerRegistry registry_;
+  bool registry_ok_{false};
+  size_t zero_copy_min_{1u << 20};
+  bool no_registry_{false};  // set while an op is captured into a hipGraph
+  uint64_t op_seq_{0};       // AllreduceImpl calls (every rank of the group counts alike)
   size_t oneshot_max_{256u << 10};
   uint64_t oneshot_ops_{0};
   bool push_{false};

@@ -88,8 +88,27 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
     if (t < n && __hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
       const unsigned long long m =
           __hip_atomic_load(mailbox(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const char *base = (m & kMailboxHeap) != 0 ? resolve.heap_base[t] : resolve.stage_base[t];
-      resolve.table[t] = base + (m & ~kMailboxHeap) + resolve.seg_off;
+      const char *src;
+      if ((m & kMailboxHeap) != 0) {
+        src = resolve.heap_base[t] + (m & ~kMailboxHeap);
+      } else if ((m & kMailboxReg) != 0) {
+        // a registered allocation of peer t: its mapping from the registry's device table (the
+        // peer only publishes one this rank acknowledged, see peer_registry.h)
+        const int slot = static_cast<int>((m >> kMailboxRegShift) & (kMaxRegs - 1));
+        const char *base = resolve.reg_table != nullptr
+                               ? resolve.reg_table[t * kMaxRegs + slot] : nullptr;
+        if (base == nullptr) {
+          // cannot happen by the protocol; fail the op (the group is rebuilt) instead of
+          // reading through a null mapping
+          __hip_atomic_store(dev_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return;
+        }
+        src = base + (m & kMailboxOffsetMask);
+      } else {
+        src = resolve.stage_base[t] + m;
+      }
+      resolve.table[t] = src + resolve.seg_off;
     }
   }
 }

@@ -24,6 +24,12 @@ Status EngineBase::EnsureDeviceComm() {
   device::DeviceGuard dg(dev_->device());
   if (dev_->ready()) return Status::kSuccess;
   const int n = GetWorldSize();
+  // Every rank brings the transports up at the same op (this is a collective), a restarted rank
+  // and the survivors of a failure alike: per-epoch decisions that must match across ranks start
+  // over here.  The host-staging trial counts ops on each rank, and a rank restarted after the
+  // survivors decided would otherwise run the trial's forms against their decided one.
+  host_stage_trial_ = 0;
+  host_stage_pipe_ = false;
   // 1. every rank describes its GPU (and exports its peer buffers when the direct transport
   //    may be used); the records travel around the host ring
   device::PeerRecord rec;
@@ -67,6 +73,7 @@ Status EngineBase::EnsureDeviceComm() {
   s = host_->Allreduce(&ok, sizeof(int), 1, coll::HostReducer(mpi::kInt, mpi::kMin));
   if (s != Status::kSuccess) return s;
   if (!ok) dev_->DropPeers();
+  if (ok) dev_->SealPeers();  // every rank mapped every registry page
   // 3. RCCL: RCCL refuses several ranks on one GPU, which the direct transport handles alone
   // (test hook rabit_mock_rccl_init_fail: every rank's communicator "fails" to come up)
   const bool want_rccl = dcfg_.algo != 2 && (!dup_gpu || mock_rccl_fail_);

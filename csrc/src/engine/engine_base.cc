@@ -147,6 +147,12 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_pipeline_chunk")) dcfg_.pipeline_chunk = core::ParseUnit(name, val);
   if (is("rabit_device_defer_second")) dcfg_.defer_second = utils::StringToBool(val);
   if (is("rabit_device_symmetric_heap")) dcfg_.sym_heap = core::ParseUnit(name, val);
+  if (is("rabit_device_zero_copy")) {
+    // a size (ordinary HBM inputs from it on are registered for in-place reads), or a boolean
+    // (0: never, 1: the default 1 MiB)
+    const size_t v = core::ParseUnit(name, val);
+    dcfg_.zero_copy_min = v == 1 ? (1u << 20) : v;
+  }
   if (is("rabit_device_user_stream")) dcfg_.ops_on_user_stream = utils::StringToBool(val);
   if (is("rabit_device_phase_timing")) dcfg_.phase_timing = utils::StringToBool(val);
   if (is("rabit_world1_fastpath")) world1_fastpath_ = utils::StringToBool(val);
@@ -202,6 +208,8 @@ void EngineBase::SetParam(const char *name, const char *val) {
 }
 
 bool EngineBase::Init(int argc, char *argv[]) {
+  // before this engine starts any thread (watchdog, copier, bring-up helpers)
+  device::DevicePlane::ConfigureRcclEnv();
   // every rabit_* environment variable is a parameter too (the reference only reads a fixed
   // list, which is kept: DMLC_* names above)
   std::vector<std::string> names = env_vars_;
@@ -831,6 +839,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_rccl\":" << (dev_ && dev_->has_comm() ? 1 : 0)
      << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
+     << ",\"zero_copy_registry\":" << (dev_ ? dev_->RegistryJson() : std::string("{}"))
      << ",\"oneshot_ops\":" << (dev_ ? dev_->oneshot_ops() : 0)
      << ",\"fused_chunks\":" << (dev_ ? dev_->fused_chunks() : 0)
      << ",\"fused_oneshots\":" << (dev_ ? dev_->fused_oneshots() : 0)

@@ -2,13 +2,17 @@
  * \file rccl_lifecycle_test.cc
  * \brief GPU test of the RCCL communicator lifecycle under failure (one MI355X is enough):
  *
- *  1. a 2-rank communicator whose second rank never joins: the non-blocking init is polled
- *     and aborted at its deadline (kTimeout), ncclCommAbort returns, and the plane builds a
- *     working one-rank communicator afterwards;
+ *  1. a 2-rank communicator whose second rank never joins: the bring-up runs on a helper
+ *     thread (RCCL's init blocks in its bootstrap while a rank is missing, whatever the
+ *     blocking flag says), the waiter gives up at the deadline (kTimeout) and abandons the
+ *     helper, and the plane builds a working one-rank communicator afterwards;
  *  2. the same, ended early by the failure probe (a peer reported dead): kAborted well before
  *     the deadline;
  *  3. an RCCL enqueue that fails (mock_rccl_error: the call returns ncclRemoteError) becomes
- *     kAborted with the communicator dropped, not a process exit, and the next epoch works.
+ *     kAborted with the communicator dropped, not a process exit, and the next epoch works;
+ *  4. three more multi-rank bring-ups that would be abandoned: the number of live abandoned
+ *     helpers stays at DevicePlane::kMaxAbandonedInits (bring-ups beyond it are refused at
+ *     once), a world-1 communicator still works, and the process exits cleanly.
  *
  * Exit status 0 when every check passes.  Reference: the survivor side of
  * `src/allreduce_robust.cc:687-725` (CheckAndRecover never waits forever on a dead peer).
@@ -65,6 +69,7 @@ bool WorldOneWorks(DevicePlane *dev) {
 
 int main() {
   setvbuf(stdout, nullptr, _IONBF, 0);  // progress survives a kill by the test's time limit
+  DevicePlane::ConfigureRcclEnv();  // as the engine does before starting threads
   DeviceConfig cfg;
   cfg.device = 0;
   cfg.comm_init_timeout_sec = 5;
@@ -119,6 +124,28 @@ int main() {
     CHECK_TRUE(!mdev.has_comm() && mdev.rccl_aborts() == 1, "communicator not aborted");
     CHECK_TRUE(WorldOneWorks(&mdev), "next epoch after the injected error");
     (void)hipFree(buf);
+  }
+  // 4. abandoned bring-ups are bounded: cases 1 and 2 left two helpers blocked in RCCL's
+  //    bootstrap; three more multi-rank bring-ups are refused at once instead of adding helpers
+  {
+    printf("[4] live abandoned helpers before: %d (cap %d)\n", DevicePlane::LiveAbandonedInits(),
+           DevicePlane::kMaxAbandonedInits);
+    CHECK_TRUE(DevicePlane::LiveAbandonedInits() == DevicePlane::kMaxAbandonedInits,
+               "live %d", DevicePlane::LiveAbandonedInits());
+    for (int i = 0; i < 3; ++i) {
+      const double t0 = Now();
+      const Status s = dev.InitComm(DevicePlane::NewUniqueId(), 2, 0, nullptr);
+      const double dt = Now() - t0;
+      printf("[4] bring-up %d: status %s after %.2f s, live abandoned %d\n", i,
+             rabit::net::StatusName(s), dt, DevicePlane::LiveAbandonedInits());
+      CHECK_TRUE(s == Status::kAborted && dt < 1.0, "status %s after %.2f s",
+                 rabit::net::StatusName(s), dt);
+      CHECK_TRUE(DevicePlane::LiveAbandonedInits() <= DevicePlane::kMaxAbandonedInits,
+                 "live %d", DevicePlane::LiveAbandonedInits());
+    }
+    CHECK_TRUE(dev.init_refused() == 3, "refused %llu",
+               static_cast<unsigned long long>(dev.init_refused()));
+    CHECK_TRUE(WorldOneWorks(&dev), "world-1 communicator after the refused bring-ups");
   }
   printf("rccl_lifecycle_test: %s (%d failures); nonblocking settles %llu\n",
          g_fail ? "FAILED" : "OK", g_fail, static_cast<unsigned long long>(dev.rccl_settled()));

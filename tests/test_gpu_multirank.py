@@ -146,6 +146,19 @@ def test_host_buffers_via_device(extra):
     assert out.count("HOSTVIADEV OK") == 3, out[-3000:]
 
 
+@pytest.mark.parametrize("mock", [["mock=1,2,1,0"], ["mock=1,2,1,0", "mock=2,3,0,0"]])
+def test_host_stage_auto_across_restart(mock):
+    """host buffers staged through HBM with rabit_host_stage=auto: a rank killed after the
+    survivors settled on a staging form comes back, and every rank still runs the same
+    collectives (the trial restarts on all ranks with the device epoch)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("host_stage_recover.py", 3, mock, attempts=4)
+    assert rc == 0, out[-5000:]
+    assert out.count("HOSTSTAGE RECOVER OK") == 3, out[-3000:]
+    assert "resumed at version" in out, out[-3000:]
+
+
 @pytest.mark.parametrize("extra", [[], ["rabit_device_symmetric_heap=160M"],
                                    ["rabit_device_fused=auto"]])
 def test_calibration_flow(extra):
@@ -163,6 +176,18 @@ def test_symmetric_zero_copy(world):
     rc, out = _run("symmetric_check.py", world)
     assert rc == 0, out[-5000:]
     assert out.count("SYMMETRIC OK") == world, out[-3000:]
+
+
+@pytest.mark.parametrize("world,args", [(2, []), (4, []), (3, ["rabit_device_direct_mode=push"]),
+                                         (2, ["rabit_device_zero_copy=0"])])
+def test_registered_zero_copy(world, args):
+    """ordinary torch allocations read in place by the peers once IPC-registered: reused,
+    offset, unaligned, freed-and-reallocated and slot-evicted buffers stay bit-exact"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("zero_copy_check.py", world, args)
+    assert rc == 0, out[-5000:]
+    assert out.count("ZEROCOPY OK") == world, out[-3000:]
 
 
 @pytest.mark.parametrize("sym", ["0", "1"])
