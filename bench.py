@@ -223,6 +223,9 @@ def run_extras(rabit, torch, dev, world):
             low = rabit.allreduce(np.array([lp[k] for k in keys]), rabit.MIN)
             out["link_probe_min_over_ranks"] = {k: round(float(v), 2) for k, v in zip(keys, low)}
         out["size_sweep"] = size_sweep(rabit, torch, dev, world)
+    # the reference speed_test's whole line: Max, Sum and a random-root Broadcast per repetition
+    phase("speed_test line")
+    out["speed_test"] = speed_test_line(rabit, torch, dev, world, (128 << 20) // 4)
     # config 3: Broadcast of a 1 GiB blob from root 0
     nb = 1 << 30
     blob = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -369,6 +372,88 @@ def time_steps(rabit, torch, x, steps, with_mean=False):
         return worst
     mean = float(rabit.allreduce(np.array([elapsed]), rabit.SUM)[0]) / rabit.get_world_size()
     return worst, mean
+
+
+def measure_ft_tax(rabit, torch, x, steps, t_robust):
+    """What fault tolerance costs on the headline op: the same 128 MiB sum on the same
+    transport and routing through rabit.probe_allreduce (outside the result log and the
+    sequence numbering), in place with the host wait as the base engine runs it, with the
+    robust engine's dual store (log slot + user buffer), and stream-ordered without the host
+    wait.  ft_tax = robust step - base op; the other two split it.  Ranks in lock step, max over
+    ranks (as time_steps)."""
+    out = {}
+    for name, mode in (("base_us", rabit.PROBE_BASE), ("dual_store_us", rabit.PROBE_DUAL_STORE),
+                       ("no_host_wait_us", rabit.PROBE_NO_WAIT)):
+        phase("ft tax %s" % name)
+        for _ in range(2):
+            rabit.probe_allreduce(x, rabit.SUM, mode)
+        torch.cuda.synchronize()
+        rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rabit.probe_allreduce(x, rabit.SUM, mode)
+        torch.cuda.synchronize()
+        rabit.allreduce(np.zeros(1, dtype=np.int32), rabit.SUM)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out[name] = round(float(rabit.allreduce(np.array([el]), rabit.MAX)[0]) / steps * 1e6, 1)
+    t_base = out["base_us"]
+    out["robust_us"] = round(t_robust * 1e6, 1)
+    out["ft_tax_us"] = round(t_robust * 1e6 - t_base, 1)
+    out["ft_tax_pct"] = round(100.0 * (t_robust * 1e6 - t_base) / (t_robust * 1e6), 1)
+    out["dual_store_cost_us"] = round(out["dual_store_us"] - t_base, 1)
+    out["host_wait_cost_us"] = round(t_base - out["no_host_wait_us"], 1)
+    out["definition"] = ("robust = the headline step; base = the same op in place with the host "
+                         "wait, outside the result log; dual_store = into a log-like slot and the "
+                         "user buffer; no_host_wait = in place, stream-ordered")
+    return out
+
+
+def speed_test_line(rabit, torch, dev, world, n, nrep=5):
+    """The reference speed_test's whole output line (test/speed_test.cc:13-99) on HBM buffers:
+    per repetition Allreduce<Max> of n float32, Allreduce<Sum> of n float32 and a Broadcast of
+    n bytes from a random root (srand(0); rand() % nproc), each rank summing its own time per
+    kind; then mean / std over ranks and speed = n * nrep * sizeof(T) / mean / 2^20 (MiB/s per
+    rank), as its PrintStats."""
+    rng = np.random.RandomState(0)
+    rank = rabit.get_rank()
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    mx = ((i * (rank + 1)) % 111).to(torch.float32)
+    sm = ((i * (rank + 1)) % 131).to(torch.float32)
+    bc = torch.empty(n, dtype=torch.uint8, device=dev)
+    del i
+    td = {"max_tdiff": 0.0, "sum_tdiff": 0.0, "bcast_tdiff": 0.0}
+
+    def timed(key, fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        td[key] += time.perf_counter() - t0
+    # one untimed round (transport bring-up, first touches), as the headline's warm-up
+    rabit.allreduce(mx, rabit.MAX)
+    rabit.allreduce(sm, rabit.SUM)
+    rabit.broadcast_tensor(bc, 0)
+    rabit.checkpoint(None)
+    t_start = time.perf_counter()
+    for _ in range(nrep):
+        root = int(rng.randint(0, 2 ** 31 - 1)) % world
+        timed("max_tdiff", lambda: rabit.allreduce(mx, rabit.MAX))
+        timed("sum_tdiff", lambda: rabit.allreduce(sm, rabit.SUM))
+        timed("bcast_tdiff", lambda: rabit.broadcast_tensor(bc, root))
+    td["tot_tdiff"] = time.perf_counter() - t_start
+    out = {}
+    for key, size in (("max_tdiff", 4), ("sum_tdiff", 4), ("bcast_tdiff", 1), ("tot_tdiff", 0)):
+        tavg = float(rabit.allreduce(np.array([td[key]]), rabit.SUM)[0]) / world
+        tsqr = float(rabit.allreduce(np.array([(td[key] - tavg) ** 2]), rabit.SUM)[0])
+        rec = {"mean_s": round(tavg, 6), "std_s": round(float(np.sqrt(tsqr / world)), 6)}
+        if size:
+            rec["speed_MiBps"] = round(n * nrep * size / tavg / 2 ** 20, 1)
+        out[key] = rec
+    out["n"], out["nrep"], out["buffers"] = n, nrep, "HBM (torch)"
+    rabit.checkpoint(None)
+    return out
 
 
 def run_config5(rabit, torch, dev, iters=5):
@@ -652,6 +737,15 @@ def main():
     HEADLINE["rank"] = rank
     HEADLINE["t"] = time.time()
     HEADLINE["rec"] = rec
+    ft_tax = None
+    if args.engine == "robust" and args.extras:
+        # the fault-tolerance tax of the headline op, on the routing the headline used
+        try:
+            rabit.set_error_mode(True)
+            rabit.checkpoint(None)
+            ft_tax = measure_ft_tax(rabit, torch, x, max(5, args.steps // 2), t_step)
+        except Exception as e:  # noqa: BLE001 - reported in the record
+            ft_tax = {"error": "%s: %s" % (type(e).__name__, e)}
 
     # side measurements after the headline: an exception is recorded, not fatal (a rank stuck
     # in one is cut off by the post-headline deadline, which still prints the headline)
@@ -673,6 +767,8 @@ def main():
         phase("extras")
         try:
             rec["extras"] = run_extras(rabit, torch, dev, world)
+            if ft_tax is not None:
+                rec["extras"]["ft_tax"] = ft_tax
             lp = rec["extras"].get("link_probe_min_over_ranks")
             if lp and lp.get("all_links_read_GBps"):
                 # the pull two-shot brings 2(n-1)/n of the buffer into every rank, so its busbw is

@@ -128,6 +128,16 @@ RABIT_DLL int RabitDevSetFused(int fused);
 RABIT_DLL int RabitDevGraphAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
                                      void *hip_stream);
 /*!
+ * \brief xrabit extension: the fault-tolerance tax, measured.  The same device allreduce the
+ *        robust engine runs (same transports and routing) but outside its result log and
+ *        sequence numbering: a collective every rank calls between the same ops, for
+ *        benchmarks.  mode 0: in place, host wait (the base engine's op); 1: into a scratch
+ *        slot and buf (the robust engine's dual store), host wait; 2: in place, stream-ordered.
+ * \return 0; -1 the op failed (no recovery: a probe); -2 no device plane
+ */
+RABIT_DLL int RabitDevProbeAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
+                                     int mode);
+/*!
  * \brief xrabit extension: per-phase hipEvent timing of the direct transport's classic two-shot
  *        allreduce (stage, barrier, reduce, barrier, gather) from now on, with fresh totals
  *        (on = 1), or off (0); averages appear in RabitGetStats as direct_phase_us.

@@ -316,6 +316,13 @@ RABIT_DLL int RabitDevSetFused(int fused) {
   return 0;
 }
 
+RABIT_DLL int RabitDevProbeAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
+                                     int mode) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) return -2;
+  return Guard([&]() { return e->DevProbeAllreduce(buf, count, enum_dtype, enum_op, mode); }, -1);
+}
+
 RABIT_DLL int RabitDevLinkProbe(size_t nbytes, double *out, int nout) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
   if (e == nullptr || out == nullptr || nout < rabit::device::PeerGroup::kLinkProbeValues) return -1;

@@ -440,7 +440,7 @@ Status EngineBase::EnsureShm() {
 }
 
 Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec,
-                                      void *dst2, int prep, double alpha) {
+                                      void *dst2, int prep, double alpha, bool host_wait) {
   const size_t bytes = spec.bytes();
   if (bytes == 0) return Status::kSuccess;
   if (dst2 == dst) dst2 = nullptr;
@@ -501,7 +501,7 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
   MaybeInjectDeviceHang();
   s = dev_->Allreduce(src, dst, dst2, spec.count, spec.dtype, spec.op, prep, alpha, MakeProbe());
   if (s != Status::kSuccess) return s;
-  return dev_->Finish(MakeProbe());
+  return dev_->Finish(MakeProbe(), host_wait);
 }
 
 Status EngineBase::TryBroadcast(void *buf, size_t size, int root, void *dev_log) {
@@ -739,6 +739,24 @@ int EngineBase::DevGraphAllreduce(void *buf, size_t count, int dtype, int op,
   if (r == -5) *why = "graph allreduce: the enqueue failed";
   if (r == 0) stats_.n_device_ops += 1;
   return r;
+}
+
+int EngineBase::DevProbeAllreduce(void *buf, size_t count, int dtype, int op, int mode) {
+  if (dev_ == nullptr) return -2;
+  utils::Check(mode >= 0 && mode <= 2, "probe allreduce: mode %d not in [0, 2]", mode);
+  utils::Check(OnDevice(buf), "probe allreduce: the buffer must be in HBM");
+  ReduceSpec spec;
+  spec.type_nbytes = coll::DTypeSize(static_cast<mpi::DataType>(dtype));
+  spec.count = count;
+  spec.dtype = dtype;
+  spec.op = op;
+  void *dst = buf, *dst2 = nullptr;
+  if (mode == 1) {
+    dst = dev_->Scratch(spec.bytes(), device::DevicePlane::kCalibScratch);
+    dst2 = buf;
+  }
+  const Status s = TryAllreduceDevice(buf, dst, spec, dst2, device::kPrepCopy, 1.0, mode != 2);
+  return s == Status::kSuccess ? 0 : -1;
 }
 
 int EngineBase::DevLinkProbe(size_t bytes, double *out) {

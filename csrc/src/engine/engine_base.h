@@ -98,6 +98,16 @@ class EngineBase : public IEngine {
                                     int prep, double alpha, const char *_file, const int _line,
                                     const char *_caller);
   /*!
+   * \brief the fault-tolerance tax, measured (RabitDevProbeAllreduce): the same device
+   *        allreduce the robust engine runs, on the same transports, but outside the result log
+   *        and the sequence numbering -- a collective every rank calls between the same ops, like
+   *        the link probe.  mode 0: in place with the host wait (what the base engine runs);
+   *        1: into a scratch slot and the user buffer (the robust engine's dual store), host
+   *        wait; 2: in place, stream-ordered (no host wait).  0 on success, -1 on failure,
+   *        -2 without the device plane.
+   */
+  int DevProbeAllreduce(void *buf, size_t count, int dtype, int op, int mode);
+  /*!
    * \brief capturable in-place RCCL allreduce (RabitDevGraphAllreduce): brings the device
    *        communicator up on first use (a collective: make the first call eagerly, on every
    *        rank), then only enqueues ncclAllReduce on `stream`.  0 or a negative code (c_api.h)
@@ -167,7 +177,8 @@ class EngineBase : public IEngine {
    *        on this rank.  prep is a device::PrepOp (kPrepCopy: none).
    */
   Status TryAllreduceDevice(const void *src, void *dst, const ReduceSpec &spec,
-                            void *dst2 = nullptr, int prep = 0, double alpha = 1.0);
+                            void *dst2 = nullptr, int prep = 0, double alpha = 1.0,
+                            bool host_wait = true);
   /*! \brief dev_log (HBM buffers only): on success the result is also in dev_log, stored by
    *  the transport itself (no copy after the collective on the direct path) */
   Status TryBroadcast(void *buf, size_t size, int root, void *dev_log = nullptr);

@@ -13,13 +13,21 @@
  * the peers' barriers / RCCL time out, the rank finds its own stream stuck after the abort and
  * exits for a restart); `mock_die_mid=...` lets the rank start the device allreduce and exit
  * in its middle, once every peer has delivered the op's first chunk to its output (survivors
- * then fail the op part-way, which must leave their input intact for the retry); `force_local`
- * and `report_stats` behave as in the reference.
+ * then fail the op part-way, which must leave their input intact for the retry);
+ * `mock_die_serving=rank,version,seqno,ntrial[,where]` kills the rank while it serves another
+ * rank's recovery (holder or relay of a replayed result, of a checkpoint load or of the
+ * bootstrap cache) during op `seqno` of `version`: where = 1 after the routing decision, 2 once
+ * the first bytes of a host transfer left, 3 right before a device exchange, 0 (default) at the
+ * first of them reached.  The reference reaches this path only when a second failure happens
+ * to coincide with a replay (`src/allreduce_robust.cc:861-973, 1037-1088, 1103-1140`);
+ * `force_local` and `report_stats` behave as in the reference.
  */
 #ifndef XRABIT_ENGINE_ENGINE_MOCK_H_
 #define XRABIT_ENGINE_ENGINE_MOCK_H_
 
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <sstream>
 #include <string>
@@ -42,6 +50,16 @@ class EngineMock : public EngineRobust {
     }
     if (!strcmp(name, "report_stats")) report_stats_ = atoi(val);
     if (!strcmp(name, "force_local")) force_local_ = atoi(val);
+    if (!strcmp(name, "mock_die_serving")) {
+      Key k;
+      int where = 0;
+      const int got = sscanf(val, "%d,%d,%d,%d,%d", &std::get<0>(k), &std::get<1>(k),
+                             &std::get<2>(k), &std::get<3>(k), &where);
+      utils::Check(got == 4 || (got == 5 && where >= 0 && where <= 3),
+                   "invalid mock_die_serving \"%s\" (expected rank,version,seqno,ntrial[,where])",
+                   val);
+      serve_map_[k] = where;
+    }
     if (!strcmp(name, "mock") || !strcmp(name, "mock_hang") || !strcmp(name, "mock_dev_hang") ||
         !strcmp(name, "mock_die_mid")) {
       Key k;
@@ -148,6 +166,20 @@ class EngineMock : public EngineRobust {
     EngineRobust::LazyCheckPoint(global_model);
   }
 
+  void ServeHook(ServePoint where) override {
+    auto it = serve_map_.find(Key(rank_, version_number_, seq_counter_, num_trial_));
+    if (it == serve_map_.end() || (it->second != 0 && it->second != static_cast<int>(where))) {
+      return;
+    }
+    static const char *names[] = {"", "routing", "data", "device exchange"};
+    fprintf(stderr, "[%d]@@@Hit Mock Die Serving (%s) at version %d seq %d\n", rank_,
+            names[static_cast<int>(where)], version_number_, seq_counter_);
+    fflush(stderr);
+    // as a crash: no unwinding through the recovery code, no Finalize
+    std::_Exit(kMockDieServingExitCode);
+  }
+  static constexpr int kMockDieServingExitCode = 249;
+
   // white-box setters for unit tests
   void TestSetState(int rank, int version, int seq) {
     rank_ = rank;
@@ -207,6 +239,7 @@ class EngineMock : public EngineRobust {
   int report_stats_{0};
   double tsum_allreduce_{0}, tsum_allgather_{0}, time_checkpoint_{0};
   std::map<Key, int> mock_map_;
+  std::map<Key, int> serve_map_;  // mock_die_serving: where (0 any)
 };
 }  // namespace engine
 }  // namespace rabit

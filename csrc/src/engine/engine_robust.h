@@ -200,6 +200,15 @@ class EngineRobust : public EngineBase {
   void CopyAny(void *dst, bool dst_dev, const void *src, bool src_dev, size_t n);
 
   // ---- recovery protocol
+  /*! \brief points where a rank serves another rank's recovery (fault injection) */
+  enum ServePoint { kServeRouting = 1, kServeData = 2, kServeDevice = 3 };
+  /*!
+   * \brief called by a rank that holds or relays recovery data for a peer (result replay,
+   *        checkpoint load, bootstrap cache): after the routing decision, after the first bytes
+   *        of a host transfer left, before a device exchange.  The mock engine kills the rank
+   *        here (mock_die_serving); no-op otherwise.
+   */
+  virtual void ServeHook(ServePoint where) { (void)where; }
   /*!
    * \brief run recovery actions preceding the requested one
    * \return true if the request was satisfied by recovery (buf holds the result),

@@ -207,6 +207,9 @@ Status EngineRobust::TryRecoverLocalState(int v) {
     device::DeviceGuard dg(dev_->device());
     s = EnsureDeviceComm();
     if (s == Status::kSuccess) {
+      bool serving = false;
+      for (const SlotCopy &c : plan) serving = serving || (c.h == rank_ && c.r != rank_);
+      if (serving) ServeHook(kServeDevice);
       size_t got = 0;
       dev_->EnterFromUser();
       s = dev_->Exchange(xs, &got, MakeProbe());

@@ -205,6 +205,7 @@ Status EngineRobust::TryDecideRouting(RecoverType role, size_t *p_size, int *p_r
   Status s = MsgPassing(std::make_pair(role == kRequestData, best_link), &req_in, &req_out,
                         DataRequest);
   if (s != Status::kSuccess) return s;
+  if (role != kRequestData) ServeHook(kServeRouting);
   p_req_in->assign(req_in.size(), false);
   for (size_t i = 0; i < req_in.size(); ++i) {
     (*p_req_in)[i] = req_in[i] != 0;
@@ -237,8 +238,13 @@ Status EngineRobust::TryRecoverData(RecoverType role, void *buf_, size_t size, i
   if (role == kPassData) src->InitRing(1, size, hcfg_.reduce_buffer_bytes);
   for (auto *l : links) l->ResetProgress();
   net::Poller poller;
+  bool sent_any = false;  // (fault injection: a server dies once its first bytes left)
   for (;;) {
     if (host_->Aborted()) return host_->Fail(nullptr, Status::kAborted);
+    if (!sent_any && role != kRequestData) {
+      for (int i = 0; i < nlink && !sent_any; ++i) sent_any = req_in[i] && links[i]->size_write > 0;
+      if (sent_any) ServeHook(kServeData);
+    }
     // bytes this node can forward so far
     const size_t avail = role == kHaveData ? size : src->size_read;
     bool done = true;
@@ -378,6 +384,7 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
       device::DeviceGuard dg(dev_->device());
       s = EnsureDeviceComm();
       if (s != Status::kSuccess) return s;
+      if (role == kHaveData) ServeHook(kServeDevice);
       size_t got = 0;
       dev_->EnterFromUser();
       s = dev_->Exchange(plan, &got, MakeProbe());
@@ -522,6 +529,7 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
   }
   s = EnsureDeviceComm();
   if (s != Status::kSuccess) return s;
+  if (holder_dev) ServeHook(kServeDevice);
   size_t got = 0;
   dev_->EnterFromUser();
   s = dev_->Exchange(plan, &got, MakeProbe());
@@ -674,11 +682,15 @@ bool EngineRobust::RecoverExec(void *buf, size_t size, int flag, int seqno, int 
       utils::Assert(!act.check_point() && !act.check_ack(),
                     "bootstrap cache restore cannot overlap a checkpoint");
       if (act.load_cache(kCache)) return false;  // everybody is a requester: nothing cached
-      if (act.diff_seq()) {
-        if (TryRestoreCache(req.load_cache(), static_cast<int>(act.seqno()),
-                            static_cast<int>(act.seqno(kCache))) != Status::kSuccess) {
-          continue;
-        }
+      // Requesters and holders are mixed: restore.  The reference restores only when the
+      // seqnos differ (allreduce_robust.cc:1281-1285), assuming a requester (seqno = its op
+      // count before LoadCheckPoint, 0) always lags the holders; survivors blocked in op 0 of a
+      // version carry seqno 0 too, and the requester then took "restored" for an empty cache
+      // and ran its bootstrap op against the survivors' op 0 (a hang; found by the chaos test,
+      // tests/test_chaos.py seed 129).
+      if (TryRestoreCache(req.load_cache(), static_cast<int>(act.seqno()),
+                          static_cast<int>(act.seqno(kCache))) != Status::kSuccess) {
+        continue;
       }
       if (req.load_cache()) return true;
       continue;

@@ -15,6 +15,7 @@ from .core import (BITOR, DTYPE_ENUM, DTYPE_ENUM__, MAX, MIN, PREP_ABS, PREP_COP
                    set_error_mode, stats, tracker_print, version_number, dump_trace,
                    checkpoint_tensors, load_checkpoint_tensors, symmetric_empty,
                    set_device_transport, set_phase_timing, allreduce_graphable, TRANSPORT_AUTO,
-                   TRANSPORT_DIRECT, TRANSPORT_RCCL, link_probe)
+                   TRANSPORT_DIRECT, TRANSPORT_RCCL, link_probe, probe_allreduce,
+                   PROBE_BASE, PROBE_DUAL_STORE, PROBE_NO_WAIT)
 
 __version__ = "0.1.0"

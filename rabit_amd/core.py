@@ -472,6 +472,27 @@ def link_probe(nbytes: int = 64 << 20) -> Optional[dict]:
     return {k: round(float(v), 2) for k, v in zip(LINK_PROBE_KEYS, out)}
 
 
+PROBE_BASE, PROBE_DUAL_STORE, PROBE_NO_WAIT = 0, 1, 2
+
+
+def probe_allreduce(t, op: int, mode: int = PROBE_BASE):
+    """The fault-tolerance tax, measured: the device allreduce the robust engine runs, on the
+    same transports and routing, but outside its result log and sequence numbering (a
+    collective every rank calls between the same ops, like link_probe; for benchmarks -- a
+    failure raises RuntimeError and is not recovered).  mode PROBE_BASE: in place with the host
+    wait, what the base engine runs; PROBE_DUAL_STORE: into a scratch slot and t, as the robust
+    engine stores into its log and the user buffer; PROBE_NO_WAIT: in place, stream-ordered."""
+    _check_init()
+    if not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
+        raise TypeError("probe_allreduce takes a contiguous HBM (cuda) tensor")
+    _sync_stream_for(t)
+    r = _LIB.RabitDevProbeAllreduce(ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                    _torch_dtype_enum(t), int(op), int(mode))
+    if r != 0:
+        raise RuntimeError("probe_allreduce failed (%d): %s" % (r, last_error()))
+    return t
+
+
 def allreduce_graphable(t, op: int):
     """In-place allreduce of an HBM tensor on the current stream, with no host-side
     synchronisation: unlike allreduce(), it can be captured into a hipGraph with the rest of

@@ -21,6 +21,10 @@ dev = torch.device("cuda", 0)
 ops = 0
 
 
+def phase(msg):
+    print("[%d] phase %s registry %s" % (rank, msg, rabit.stats()["zero_copy_registry"]), flush=True)
+
+
 def check(x, tag, seed):
     """allreduce(SUM) of (base + seed + rank) into x, compare with the closed form"""
     global ops
@@ -37,12 +41,14 @@ def check(x, tag, seed):
 x = torch.empty(5 << 20, dtype=torch.float32, device=dev)
 for it in range(8):
     check(x, "reuse", it)
+phase("reuse done")
 st = rabit.stats()
 reg1 = st["zero_copy_registry"]
 # 2. views into the same allocation: aligned offset (zero copy), unaligned (staged)
 for it in range(4):
     check(x[4096:4096 + (2 << 20)], "view", 100 + it)
     check(x[3:3 + (2 << 20)], "unaligned", 200 + it)
+phase("views done")
 # 3. free the segment and allocate again (same size: often the same address, new buffer id)
 del x
 torch.cuda.synchronize()
@@ -53,11 +59,13 @@ for it in range(6):
 del y
 torch.cuda.synchronize()
 torch.cuda.empty_cache()
+phase("realloc done")
 # 4. 40 live allocations (> 32 registry slots) of 12 MiB, each its own segment, cycled twice
 bufs = [torch.empty(3 << 20, dtype=torch.float32, device=dev) for _ in range(40)]
 for rnd in range(2):
     for i, b in enumerate(bufs):
         check(b, "cycle", 1000 + 50 * rnd + i)
+phase("cycle done")
 # 5. other dtypes and MAX on a reused buffer
 z = torch.empty(3 << 20, dtype=torch.int32, device=dev)
 for it in range(4):

@@ -64,6 +64,34 @@ def test_headline_value_is_busbw_above_one_rank():
     assert one["value_is"].startswith("algbw")
 
 
+def test_ft_tax_fields_cpu():
+    """measure_ft_tax's arithmetic on a stand-in engine (CPU): ft_tax = robust step - base op,
+    dual-store and host-wait costs relative to the base op, times max over ranks"""
+    import importlib
+    import types
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    clock = {"t": 0.0}
+    cost = {0: 100e-6, 1: 130e-6, 2: 90e-6}
+    rabit = types.SimpleNamespace(PROBE_BASE=0, PROBE_DUAL_STORE=1, PROBE_NO_WAIT=2, SUM=2, MAX=0)
+
+    def probe(x, op, mode):
+        clock["t"] += cost[mode]
+    rabit.probe_allreduce = probe
+    rabit.allreduce = lambda a, op: np.asarray(a)
+    torch = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda: None))
+    real = bench.time.perf_counter
+    bench.time.perf_counter = lambda: clock["t"]
+    try:
+        ft = bench.measure_ft_tax(rabit, torch, None, 10, 150e-6)
+    finally:
+        bench.time.perf_counter = real
+    assert ft["base_us"] == 100.0 and ft["dual_store_us"] == 130.0 and ft["no_host_wait_us"] == 90.0
+    assert ft["ft_tax_us"] == 50.0 and abs(ft["ft_tax_pct"] - 33.3) < 0.1
+    assert ft["dual_store_cost_us"] == 30.0 and ft["host_wait_cost_us"] == 10.0
+
+
 def test_bench_torchrun_busbw_and_config5():
     """GPU: bench.py under torch.distributed.run with 2 ranks sharing the box's GPU (the direct
     transport carries the data): the headline `value` is the busbw, and the extras carry
@@ -94,6 +122,17 @@ def test_bench_torchrun_busbw_and_config5():
     ex = rec["extras"]
     assert ex["config5_iter_us"] > 0 and ex["config5_sum_only_iter_us"] > 0, ex
     assert "config5_ckpt_overhead_us" in ex, ex
+    # the fault-tolerance tax of the headline op and the reference speed_test's whole line
+    ft = ex["ft_tax"]
+    assert "error" not in ft, ft
+    for k in ("base_us", "dual_store_us", "no_host_wait_us", "robust_us", "ft_tax_us",
+              "ft_tax_pct", "dual_store_cost_us", "host_wait_cost_us"):
+        assert k in ft, (k, ft)
+    assert ft["base_us"] > 0 and ft["robust_us"] > 0, ft
+    st = ex["speed_test"]
+    for k in ("max_tdiff", "sum_tdiff", "bcast_tdiff"):
+        assert st[k]["speed_MiBps"] > 0 and st[k]["mean_s"] > 0, st
+    assert st["tot_tdiff"]["mean_s"] > 0, st
 
 
 test_bench_torchrun_busbw_and_config5.pytestmark = [__import__("pytest").mark.gpu]

@@ -32,6 +32,10 @@ SCENARIOS = {
     "local_recover_force_local": (["mode=local", "force_local=1"] + LOCAL, 3),
     "lazy_recover_die_hard": (["mode=lazy"] + DIE_HARD, 4),
     "lazy_recover_die_same": (["mode=lazy"] + DIE_SAME, 3),
+    # a death in op 0 of a version with the bootstrap cache on: the survivors' seqno (0)
+    # equals the restarted rank's bootstrap seqno (found by tests/test_chaos.py, seed 129)
+    "bootstrap_cache_kill_at_op0": (["mode=global", "rabit_bootstrap_cache=1", "mock=8,1,0,0",
+                                     "mock=3,2,0,0"], 2),
     "ringallreduce": (["mode=global", "rabit_reduce_ring_mincount=10"], 0),
     "tree_only_small_buffer": (["mode=global", "rabit_reduce_ring_mincount=100000",
                                 "rabit_reduce_buffer=4K", "rabit_tree_reduce_minsize=1K"] + DIE, 2),
