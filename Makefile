@@ -4,6 +4,8 @@
 #
 #   make -j8            libraries (robust/base/mock/empty flavours, same names as rabit)
 #   make tests          C++ unit-test and integration programs in build/bin
+#   make lint           style / hygiene checks of C++, HIP and Python (tools/lint.py)
+#   make doc            API reference docs/api.md from the sources (tools/gendoc.py)
 #   make clean
 
 ROCM      ?= /opt/rocm
@@ -22,7 +24,8 @@ INC       := -Icsrc/include -Icsrc/src -I$(ROCM)/include
 CXXFLAGS  := $(OPT) -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread \
              -D__HIP_PLATFORM_AMD__ $(INC) $(SAN)
 HIPFLAGS  := $(OPT) -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(INC)
-LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrccl -lrocprofiler-sdk-roctx -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
+# -z defs: a symbol declared but never defined fails the link, not the first dlopen
+LDLIBS    := -Wl,-z,defs -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrccl -lrocprofiler-sdk-roctx -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
 
 CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc csrc/src/net/link_reset.cc \
              csrc/src/coll/host_coll.cc csrc/src/coll/shm_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc csrc/src/device/dma_copier.cc csrc/src/device/peer_coll.cc csrc/src/device/peer_registry.cc csrc/src/device/host_stager.cc \
@@ -39,7 +42,7 @@ HEADERS   := $(shell find csrc -name '*.h')
 FLAVOURS  := rabit rabit_base rabit_mock rabit_empty
 LIBS      := $(foreach f,$(FLAVOURS),$(LIBDIR)/lib$(f).so) $(LIBDIR)/librabit_mock.a
 
-.PHONY: all libs tests clean asan tsan
+.PHONY: all libs tests clean asan tsan lint doc
 all: libs
 libs: $(LIBS)
 
@@ -109,6 +112,13 @@ asan:
 	  libs tests
 tsan:
 	$(MAKE) BUILD=build/tsan LIBDIR=build/tsan/lib OPT=-O1 SAN="-fsanitize=thread" libs tests
+
+# the reference's `make lint` / `make doc` (Makefile:97-104) ran cpplint / pylint and
+# Doxygen / Sphinx, none of which this image has: tools/lint.py and tools/gendoc.py do the job
+lint:
+	python3 tools/lint.py
+doc:
+	python3 tools/gendoc.py
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR)/*.so $(LIBDIR)/*.a

@@ -23,8 +23,9 @@ Rank 0 prints one JSON line.  `value` is BASELINE.json's metric, the allreduce B
 N > 1.  At N = 1 busbw is 0 by definition (no byte crosses a link), so `value` is the algbw of
 the robust engine's local op and `collective` is false; `value_is` names which one it is.  The
 per-step wall clock, algbw, the whole-job aggregate N * S / t and the reference's own
-`sum_tdiff-speed` (per-rank MiB/s, test/speed_test.cc:52-69) are reported alongside.  The whole run is under a wall-clock deadline
-(--deadline): a rank that exceeds it names the phase it was in and exits non-zero.  The side
+`sum_tdiff-speed` (per-rank MiB/s, test/speed_test.cc:52-69) are reported alongside.  The whole
+run is under a wall-clock deadline (--deadline): a rank that exceeds it names the phase it was in
+and exits non-zero.  The side
 measurements after the headline (variants, extras) have a budget of their own (--post-deadline)
 and cannot take the measured headline with them: an exception in one is recorded in
 `post_headline_failure`, and a rank stuck in one ends the run with the headline printed.
@@ -65,7 +66,8 @@ def start_deadline(seconds, rank, post_seconds):
                 break
             time.sleep(min(1.0, limit - now))
         sys.stderr.write("bench.py: rank %d exceeded its deadline in phase '%s' "
-                         "(%.0f s into the run)\n" % (rank, PHASE["name"], time.time() - PHASE["t0"]))
+                         "(%.0f s into the run)\n"
+                         % (rank, PHASE["name"], time.time() - PHASE["t0"]))
         sys.stderr.flush()
         if HEADLINE["rec"] is not None:
             emit_headline("deadline in phase '%s'" % PHASE["name"])
@@ -173,34 +175,41 @@ def calibrated_mode(st):
 
 
 def size_sweep(rabit, torch, dev, world):
-    """N > 1: float32 sum latency from 4 KiB to 16 MiB on each transport that is up (median of
-    10, ranks in lock step, max over ranks) -- the data behind the size routing; the calibrated
-    routing is restored afterwards"""
-    st0 = rabit.stats()
+    """N > 1: float32 sum latency from 4 KiB to 128 MiB on each transport and direct form that
+    is up (median of 10, ranks in lock step, max over ranks), and on the calibrated routing --
+    the data behind the size routing.  routed_over_best: the routed time over the best forced
+    variant per size (1.0 = the routing picked the fastest).  The calibrated routing is restored
+    afterwards."""
     out = {}
-    for name, which in (("rccl", rabit.TRANSPORT_RCCL), ("direct", rabit.TRANSPORT_DIRECT),
-                        ("routed", rabit.TRANSPORT_AUTO)):
+    sizes = (4 << 10, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 32 << 20, 128 << 20)
+    legs = (("rccl", rabit.TRANSPORT_RCCL, None), ("direct-pull", rabit.TRANSPORT_DIRECT, "pull"),
+            ("direct-push", rabit.TRANSPORT_DIRECT, "push"),
+            ("direct-pipelined", rabit.TRANSPORT_DIRECT, "pipelined"),
+            ("routed", rabit.TRANSPORT_AUTO, None))
+    xs = {nb: torch.ones(nb // 4, dtype=torch.float32, device=dev) for nb in sizes}
+    for name, which, mode in legs:
         phase("sweep %s" % name)
-        up = rabit.set_device_transport(which, None)
-        if which == rabit.TRANSPORT_DIRECT and up:
-            # the calibrated direct form
-            up = rabit.set_device_transport(which, calibrated_mode(st0),
-                                            bool(st0.get("direct_fused")))
+        up = rabit.set_device_transport(which, mode)
         up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
         if not up:
             continue
         row = {}
-        for nbytes in (4 << 10, 64 << 10, 1 << 20, 16 << 20):
-            x = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        for nbytes in sizes:
+            x = xs[nbytes]
             rabit.allreduce(x, rabit.SUM)
             row[str(nbytes)] = round(_timed(rabit, torch, lambda: rabit.allreduce(x, rabit.SUM),
                                             10) * 1e6, 1)
+            rabit.checkpoint(None)
         out[name + "_us"] = row
-        rabit.checkpoint(None)
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
-    if st0.get("device_direct"):
-        rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
-                                   bool(st0.get("direct_fused")))
+    del xs
+    routed = out.get("routed_us")
+    if routed:
+        ratio = {}
+        for k, t in routed.items():
+            best = min([v[k] for n, v in out.items() if n != "routed_us" and k in v] or [t])
+            ratio[k] = round(t / best, 3) if best > 0 else None
+        out["routed_over_best"] = ratio
     return out
 
 
@@ -245,9 +254,6 @@ def run_extras(rabit, torch, dev, world):
         for name, which in (("rccl", rabit.TRANSPORT_RCCL), ("direct", rabit.TRANSPORT_DIRECT)):
             phase("broadcast %s" % name)
             up = rabit.set_device_transport(which, None)
-            if which == rabit.TRANSPORT_DIRECT and up:
-                up = rabit.set_device_transport(which, calibrated_mode(st0),
-                                                bool(st0.get("direct_fused")))
             up = not rabit.allreduce(np.array([0 if up else 1], dtype=np.int32), rabit.MAX)[0]
             if not up:
                 continue
@@ -259,13 +265,11 @@ def run_extras(rabit, torch, dev, world):
                          "check": good}
             rabit.checkpoint(None)
         rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
-        if st0.get("device_direct"):
-            rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
-                                       bool(st0.get("direct_fused")))
         out["broadcast_1GiB_by_transport"] = per
         st1 = rabit.stats()
         out["broadcast_routing"] = {"calibration_us": dict(zip(
-            ["rccl_64KiB", "rccl_big", "direct_64KiB", "direct_big"], st1.get("calib_bcast_us", []))),
+            ["rccl_64KiB", "rccl_big", "direct_64KiB", "direct_big"],
+            st1.get("calib_bcast_us", []))),
             "direct_min_bytes": st1.get("bcast_direct_min"),
             "direct_below_bytes": st1.get("bcast_direct_below"),
             "direct_bcast_chunks": st1.get("direct_bcast_chunks")}
@@ -294,8 +298,8 @@ def run_extras(rabit, torch, dev, world):
     rabit.allreduce(hb, rabit.SUM)
     t = _timed(rabit, torch, lambda: rabit.allreduce(hb, rabit.SUM), 5)
     out["allreduce_128MiB_bf16_us"] = round(t * 1e6, 1)
-    out["allreduce_128MiB_bf16_busbw_GBps"] = (round((128 << 20) / t / 1e9 * 2 * (world - 1) / world, 2)
-                                               if world > 1 else None)
+    out["allreduce_128MiB_bf16_busbw_GBps"] = (
+        round((128 << 20) / t / 1e9 * 2 * (world - 1) / world, 2) if world > 1 else None)
     rabit.checkpoint(None)
     del hb
     # the reference's own benchmark shape (test/speed_test.cc): 128 MiB float32 in HOST memory.
@@ -350,7 +354,8 @@ def bandwidths(world, size_bytes, t_step):
     if world > 1:
         out["value"], out["value_is"] = out["busbw_GBps"], "busbw_GBps"
     else:
-        out["value"], out["value_is"] = out["algbw_GBps"], "algbw_GBps (N=1: busbw is 0 by definition)"
+        out["value"] = out["algbw_GBps"]
+        out["value_is"] = "algbw_GBps (N=1: busbw is 0 by definition)"
     return out
 
 
@@ -553,9 +558,6 @@ def run_variants(rabit, torch, dev, n, world, rank, ref, steps, forced_rccl=Fals
         rabit.set_device_transport(rabit.TRANSPORT_RCCL, None)
         return out, phases
     rabit.set_device_transport(rabit.TRANSPORT_AUTO, None)
-    if st0.get("device_direct"):
-        rabit.set_device_transport(rabit.TRANSPORT_AUTO, calibrated_mode(st0),
-                                   bool(st0.get("direct_fused")))
     return out, phases
 
 
@@ -733,7 +735,8 @@ def main():
                           "per-op bookkeeping plus its HBM result-log copy (robust-path overhead, "
                           "not a collective)")
     if shared_gpu:
-        rec["shared_gpu_rehearsal"] = "%d ranks on %d GPU(s): not an xGMI measurement" % (world, ngpu)
+        rec["shared_gpu_rehearsal"] = ("%d ranks on %d GPU(s): not an xGMI measurement"
+                                       % (world, ngpu))
     HEADLINE["rank"] = rank
     HEADLINE["t"] = time.time()
     HEADLINE["rec"] = rec

@@ -134,7 +134,8 @@ class IEngine {
   virtual std::string GetHost() const = 0;
   virtual void TrackerPrint(const std::string &msg) = 0;
   // ---------------- xrabit extensions ----------------
-  /*! \brief HIP stream (hipStream_t) that device collectives are ordered after; nullptr = null stream */
+  /*! \brief HIP stream (hipStream_t) that device collectives are ordered after;
+   *  nullptr = null stream */
   virtual void SetStream(void *stream) { (void)stream; }
   /*! \brief HIP device ordinal used by this engine, -1 when there is no device plane */
   virtual int GetDevice() const { return -1; }

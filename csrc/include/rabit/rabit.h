@@ -129,7 +129,8 @@ class Reducer {
 
 /*!
  * \brief reducer for variable-size objects serialized into fixed max_nbyte slots.
- *        DType must provide Load(Stream*), Save(Stream*) const and Reduce(const DType&, size_t max_nbyte).
+ *        DType must provide Load(Stream*), Save(Stream*) const and Reduce(const DType&, size_t
+ * max_nbyte).
  */
 template <typename DType>
 class SerializeReducer {

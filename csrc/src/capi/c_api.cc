@@ -278,6 +278,11 @@ RABIT_DLL int RabitDevSetTransport(int which, int direct_mode) {
   if (which == 0 && !d->has_comm()) return -1;
   if (which == 1 && !d->has_peers()) return -1;
   if (direct_mode != 0 && !d->has_peers()) return -1;
+  if (which < 0 && direct_mode == 0) {
+    // back to the calibrated routing: transport and direct form per size band
+    d->RestoreCalibrated();
+    return 0;
+  }
   d->ForceTransport(which);
   if (direct_mode != 0) {
     // 1 pull, 2 push, 3 the pipelined push form
@@ -325,7 +330,9 @@ RABIT_DLL int RabitDevProbeAllreduce(void *buf, size_t count, int enum_dtype, in
 
 RABIT_DLL int RabitDevLinkProbe(size_t nbytes, double *out, int nout) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
-  if (e == nullptr || out == nullptr || nout < rabit::device::PeerGroup::kLinkProbeValues) return -1;
+  if (e == nullptr || out == nullptr || nout < rabit::device::PeerGroup::kLinkProbeValues) {
+    return -1;
+  }
   return Guard([&]() { return e->DevLinkProbe(nbytes, out); }, -1);
 }
 

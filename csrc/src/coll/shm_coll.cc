@@ -189,7 +189,9 @@ Status ShmGroup::Allreduce(const void *src_, void *dst_, size_t tn, size_t count
     for (int q = 0; q < n_; ++q) {
       if (q == rank_) continue;
       const size_t qlo = std::min(c, seg * q), qhi = std::min(c, qlo + seg);
-      if (qhi > qlo) std::memcpy(dst + (off + qlo) * tn, stage(q, which) + qlo * tn, (qhi - qlo) * tn);
+      if (qhi > qlo) {
+        std::memcpy(dst + (off + qlo) * tn, stage(q, which) + qlo * tn, (qhi - qlo) * tn);
+      }
     }
   }
   ++ops_;

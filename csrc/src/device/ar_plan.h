@@ -96,7 +96,8 @@ struct ArPipeline {
   size_t len(size_t k) const { return std::min(chunk, count - k * chunk); }
   /*! \brief segment q of chunk k: [lo, hi) within the chunk (whole 256-element blocks) */
   void seg_range(size_t k, int q, size_t *lo, size_t *hi) const {
-    const size_t s = ((len(k) + static_cast<size_t>(n) - 1) / static_cast<size_t>(n) + 255) / 256 * 256;
+    const size_t nn = static_cast<size_t>(n);
+    const size_t s = ((len(k) + nn - 1) / nn + 255) / 256 * 256;
     *lo = std::min(len(k), s * static_cast<size_t>(q));
     *hi = std::min(len(k), *lo + s);
   }

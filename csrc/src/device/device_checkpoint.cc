@@ -247,7 +247,9 @@ void DeviceCheckpoint::LoaderImpl::Load(Stream *fi) {
   utils::Check(n == ptrs.size(), "device checkpoint holds %llu buffers, %zu given",
                static_cast<unsigned long long>(n), ptrs.size());
   std::vector<uint64_t> sizes(n);
-  for (auto &s : sizes) utils::Check(fi->Read(&s, sizeof(s)) == sizeof(s), "device checkpoint: size");
+  for (auto &s : sizes) {
+    utils::Check(fi->Read(&s, sizeof(s)) == sizeof(s), "device checkpoint: size");
+  }
   owner->loader_active_ = false;
   if (owner->payload_delivered_) {
     // the engine already broadcast the payloads into ptrs on the device
@@ -260,7 +262,8 @@ void DeviceCheckpoint::LoaderImpl::Load(Stream *fi) {
   }
   std::vector<char> host;
   for (size_t i = 0; i < n; ++i) {
-    utils::Check(sizes[i] == nbytes[i], "device checkpoint buffer %zu: %llu bytes stored, %zu given",
+    utils::Check(sizes[i] == nbytes[i],
+                 "device checkpoint buffer %zu: %llu bytes stored, %zu given",
                  i, static_cast<unsigned long long>(sizes[i]), nbytes[i]);
     host.resize(sizes[i]);
     if (sizes[i] == 0) continue;

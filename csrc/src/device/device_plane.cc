@@ -735,6 +735,11 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_pipeline_chunk(cfg_.pipeline_chunk);
     peers_->set_defer_second(cfg_.defer_second);
     peers_->set_zero_copy_min(cfg_.zero_copy_min);
+    // a new group starts from the configured form; a calibration (or its adoption) replaces it
+    SetDefaultForm(cfg_.direct_mode == 2, cfg_.pipeline_mode == 1, cfg_.fused_mode == 1);
+    transport_bands_.clear();
+    form_bands_.clear();
+    form_forced_ = false;
   } catch (const std::exception &e) {
     peers_.reset();
     *why = e.what();
@@ -1010,6 +1015,7 @@ Status DevicePlane::Allreduce(const void *send, void *recv, void *recv2, size_t 
   const size_t bytes = count * TypeBytes(dtype);
   op_bytes_ = bytes;
   if (UseDirect(bytes)) {
+    ApplyForm(bytes);
     CheckHip(peers_->Allreduce(send, recv, recv2, count, dtype, op, prep, alpha),
              "direct allreduce");
     return Status::kSuccess;
@@ -1081,6 +1087,7 @@ int DevicePlane::GraphAllreduce(void *buf, size_t count, int dtype, int op, hipS
   if (count == 0) return 0;
   DeviceGuard dg(device_);
   if (peers_ != nullptr && (comm_ == nullptr || UseDirect(count * TypeBytes(dtype)))) {
+    ApplyForm(count * TypeBytes(dtype));
     // the direct transport's classic form, barriers numbered on the device (replayable)
     graph_direct_ops_ += 1;
     return peers_->AllreduceGraphable(buf, count, dtype, op, stream) == hipSuccess ? 0 : -5;
@@ -1106,6 +1113,7 @@ Status DevicePlane::AllreduceCustom(const void *send, void *recv, void *recv2, s
   const size_t bytes = count * type_nbytes;
   op_bytes_ = bytes;
   if (UseDirect(bytes)) {
+    ApplyForm(bytes);
     PeerGroup::ReduceStep step = [launcher](void *dst, const void *const *srcs, int n, size_t c,
                                             const int *guard, const void *const *, double,
                                             hipStream_t st) {
@@ -1150,9 +1158,9 @@ Status DevicePlane::AllreduceByKernel(const void *send, void *recv, size_t count
   for (const std::vector<int> &p : plan.ReducePasses(rank_, kMaxReduceSources)) {
     srcs.clear();
     for (int k : p) {
-      srcs.push_back(k < 0 ? static_cast<const void *>(dst)
-                           : (k == rank_ ? static_cast<const void *>(in + plan.lo(rank_) * tn)
-                                         : inbox + static_cast<size_t>(k) * plan.slot_bytes(rank_)));
+      const void *own = in + plan.lo(rank_) * tn;
+      const void *slot = inbox + static_cast<size_t>(k) * plan.slot_bytes(rank_);
+      srcs.push_back(k < 0 ? static_cast<const void *>(dst) : (k == rank_ ? own : slot));
     }
     CheckHip(pass(dst, srcs.data(), static_cast<int>(srcs.size()), plan.elems(rank_), p[0] < 0,
                   stream_),

@@ -81,7 +81,8 @@ struct DeviceConfig {
   // host-buffer allreduce staged through HBM (rabit_host_via_device): pipelined in chunks of
   // this size through pinned slots (host_stager.h), or one whole copy each way (0)
   size_t host_stage_chunk{16u << 20};
-  int host_stage_threads{0};           // memcpy threads of the staging (0: host share / local ranks)
+  int host_stage_threads{0};           // memcpy threads of the staging (0: host share /
+                                       // local ranks)
   int host_stage_streams{3};           // 3: H2D / collective / D2H on separate streams; 1: all on
                                        // the plane stream
   int rccl_min_ctas{0};                // ncclConfig_t minCTAs / maxCTAs (0: RCCL's choice)
@@ -256,15 +257,53 @@ class DevicePlane {
   bool UseDirect(size_t bytes) const {
     if (peers_ == nullptr) return false;
     if (force_ >= 0) return force_ == 1;
-    return comm_ == nullptr || cfg_.algo == 2 || bytes >= cfg_.direct_min_bytes ||
-           bytes < direct_below_bytes_;
+    if (comm_ == nullptr || cfg_.algo == 2) return true;
+    if (!transport_bands_.empty()) return BandAt(transport_bands_, bytes).direct != 0;
+    return bytes >= cfg_.direct_min_bytes || bytes < direct_below_bytes_;
+  }
+  /*! \brief what the calibration chose for one band of op sizes: the transport, and the form of
+   *  the direct two-shot path */
+  struct RouteChoice {
+    size_t lo;  // ops of at least lo bytes (up to the next band)
+    int8_t direct, push, pipeline, fused;
+  };
+  /*!
+   * \brief the calibrated piecewise routing (engine/routing.h): transport bands (direct or
+   *        RCCL per size) and form bands (the fastest direct form per size, used whenever an op
+   *        goes direct).  Empty vectors: the two-threshold routing and one fixed form.  Clears
+   *        a forced form.
+   */
+  void SetRoutes(const std::vector<RouteChoice> &transport, const std::vector<RouteChoice> &form) {
+    transport_bands_ = transport;
+    form_bands_ = form;
+    form_forced_ = false;
+  }
+  const std::vector<RouteChoice> &transport_bands() const { return transport_bands_; }
+  const std::vector<RouteChoice> &form_bands() const { return form_bands_; }
+  /*! \brief back to the calibrated transport and form (undo ForceTransport / forced forms) */
+  void RestoreCalibrated() {
+    force_ = -1;
+    form_forced_ = false;
+    if (peers_ != nullptr && form_bands_.empty()) {
+      peers_->set_push(default_form_.push != 0);
+      peers_->set_pipeline(default_form_.pipeline != 0);
+      peers_->set_fused(default_form_.fused != 0);
+    }
+  }
+  const RouteChoice &default_form() const { return default_form_; }
+  /*! \brief the form used when no form bands exist (the configured or calibrated one) */
+  void SetDefaultForm(bool push, bool pipeline, bool fused) {
+    default_form_ = RouteChoice{0, 1, static_cast<int8_t>(push), static_cast<int8_t>(pipeline),
+                                static_cast<int8_t>(fused)};
   }
   /*! \brief route a broadcast of this many bytes over the direct transport: by its own
    *  calibration once that ran (a broadcast moves each byte once per link, an allreduce twice,
    *  so the crossover differs), by the allreduce routing before */
   bool UseDirectBcast(size_t bytes) const {
     if (peers_ == nullptr) return false;
-    if (force_ >= 0 || !bcast_routed_ || comm_ == nullptr || cfg_.algo == 2) return UseDirect(bytes);
+    if (force_ >= 0 || !bcast_routed_ || comm_ == nullptr || cfg_.algo == 2) {
+      return UseDirect(bytes);
+    }
     return bytes >= bcast_min_bytes_ || bytes < bcast_below_bytes_;
   }
   void set_bcast_routing(size_t min_bytes, size_t below_bytes) {
@@ -293,12 +332,14 @@ class DevicePlane {
   int rccl_min_ctas() const { return cfg_.rccl_min_ctas; }
   /*! \brief direct reduce-scatter by remote writes (push) instead of remote reads */
   void SetDirectPush(bool v) {
+    form_forced_ = true;
     if (peers_ != nullptr) peers_->set_push(v);
   }
   bool direct_push() const { return peers_ != nullptr && peers_->push(); }
   uint64_t push_chunks() const { return peers_ ? peers_->push_chunks() : 0; }
   /*! \brief direct two-shot allreduces as the pipelined push form (with SetDirectPush(true)) */
   void SetPipeline(bool v) {
+    form_forced_ = true;
     if (peers_ != nullptr) peers_->set_pipeline(v);
   }
   bool pipeline() const { return peers_ != nullptr && peers_->pipeline(); }
@@ -342,6 +383,7 @@ class DevicePlane {
   uint64_t fused_chunks() const { return peers_ ? peers_->fused_chunks() : 0; }
   uint64_t fused_oneshots() const { return peers_ ? peers_->fused_oneshots() : 0; }
   void SetFused(bool v) {
+    form_forced_ = true;
     if (peers_ != nullptr) peers_->set_fused(v);
   }
   bool fused() const { return peers_ != nullptr && peers_->fused(); }
@@ -503,7 +545,8 @@ class DevicePlane {
   /*! \brief count one RCCL enqueue; true when the mock_rccl_error hook makes it fail */
   bool MockRcclFault();
   /*! \brief one grouped ncclSend / ncclRecv call over ops (pointers from at(i, op)) */
-  Status RunP2P(const std::vector<P2POp> &ops, const std::function<char *(size_t, const P2POp &)> &at,
+  Status RunP2P(const std::vector<P2POp> &ops,
+                const std::function<char *(size_t, const P2POp &)> &at,
                 const char *what, const FailureProbe &probe);
   /*! \brief one reduce pass of the kernel-reduced allreduce: dst = reduce(srcs) over count
    *  elements; acc_first: srcs[0] is the running result of an earlier pass (not prepared) */
@@ -515,8 +558,25 @@ class DevicePlane {
   Status AllreduceByKernel(const void *send, void *recv, size_t count, size_t type_nbytes,
                            const PassFn &pass, const FailureProbe &probe);
 
+  static const RouteChoice &BandAt(const std::vector<RouteChoice> &bands, size_t bytes) {
+    size_t i = 0;
+    while (i + 1 < bands.size() && bytes >= bands[i + 1].lo) ++i;
+    return bands[i];
+  }
+  /*! \brief a direct op of this size is about to run: its calibrated form, unless forced */
+  void ApplyForm(size_t bytes) {
+    if (form_forced_ || form_bands_.empty() || peers_ == nullptr) return;
+    const RouteChoice &c = BandAt(form_bands_, bytes);
+    peers_->set_push(c.push != 0);
+    peers_->set_pipeline(c.pipeline != 0);
+    peers_->set_fused(c.fused != 0);
+  }
+
   DeviceConfig cfg_;
   int device_{-1};
+  std::vector<RouteChoice> transport_bands_, form_bands_;
+  RouteChoice default_form_{0, 1, 0, 0, 0};
+  bool form_forced_{false};
   hipStream_t stream_{nullptr};       // stream collectives are enqueued on
   hipStream_t own_stream_{nullptr};   // private non-blocking stream (ops_on_user_stream=false)
   hipStream_t user_stream_{nullptr};

@@ -149,7 +149,8 @@ __device__ __forceinline__ bool Await(const FusedAllreduceArgs &a, int *s_bad, i
  *  the peer with no L2 write-back of this XCD (MI355X_MICROARCH.md, inter-workgroup visibility;
  *  cdna_hip_programming.md Guideline 16 R1, at system instead of agent scope) */
 template <bool REMOTE>
-__device__ __forceinline__ void StoreStage(uint4 *dv, __amdgpu_buffer_rsrc_t rs, size_t v, uint4 x) {
+__device__ __forceinline__ void StoreStage(uint4 *dv, __amdgpu_buffer_rsrc_t rs, size_t v,
+                                           uint4 x) {
   if (REMOTE) {
     u32x4_t w = {x.x, x.y, x.z, x.w};
     __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(v * 16), 0, kCpolSystem);
@@ -191,7 +192,9 @@ __device__ __forceinline__ bool CopyPrep(T *d, const T *s, size_t n, int prep, T
       StoreStage<REMOTE>(dv, rs, v, prep == kPrepCopy ? sv[v] : PrepVec<T>(sv[v], prep, alpha));
     }
   }
-  for (size_t e = nvec * L + threadIdx.x; e < n; e += kBlock) d[e] = PrepApply<T>(s[e], prep, alpha);
+  for (size_t e = nvec * L + threadIdx.x; e < n; e += kBlock) {
+    d[e] = PrepApply<T>(s[e], prep, alpha);
+  }
   return nvec * L < n;
 }
 

@@ -163,15 +163,18 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
     uint4 x[NSRC][U];
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) {
+      const uint4 *sk = reinterpret_cast<const uint4 *>(Src(srcs, k));
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[k][u] = reinterpret_cast<const uint4 *>(Src(srcs, k))[base + u * kBlock];
+      for (int u = 0; u < U; ++u) x[k][u] = sk[base + u * kBlock];
     }
     if (srcs.prep != 0) {  // uniform branch: the fused lazy prepare, applied on load
 #pragma unroll
       for (int k = 0; k < NSRC; ++k) {
         if (k < srcs.prep_from) continue;
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[k][u] = PrepVec<T>(x[k][u], srcs.prep, static_cast<T>(srcs.prep_alpha));
+        for (int u = 0; u < U; ++u) {
+          x[k][u] = PrepVec<T>(x[k][u], srcs.prep, static_cast<T>(srcs.prep_alpha));
+        }
       }
     }
 #pragma unroll

@@ -125,7 +125,9 @@ PeerGroup::~PeerGroup() {
     for (auto &e : ev_) (void)hipEventDestroy(e);
   }
   for (size_t r = 0; r < peer_base_.size(); ++r) {
-    if (peer_base_[r] != nullptr && peer_base_[r] != base_) (void)hipIpcCloseMemHandle(peer_base_[r]);
+    if (peer_base_[r] != nullptr && peer_base_[r] != base_) {
+      (void)hipIpcCloseMemHandle(peer_base_[r]);
+    }
   }
   for (size_t r = 0; r < peer_heap_.size(); ++r) {
     if (peer_heap_[r] != nullptr && peer_heap_[r] != heap_.base) {
@@ -932,7 +934,9 @@ hipError_t PeerGroup::Exchange(const std::vector<ExchangeItem> &plan, size_t *by
   }
   XRABIT_TRY_HIP(flush());
   size_t rounds = 0;
-  for (int s = 0; s < n_; ++s) rounds = std::max(rounds, (stream_len[s] + stage_bytes_ - 1) / stage_bytes_);
+  for (int s = 0; s < n_; ++s) {
+    rounds = std::max(rounds, (stream_len[s] + stage_bytes_ - 1) / stage_bytes_);
+  }
   for (size_t r = 0; r < rounds; ++r) {
     const size_t lo = r * stage_bytes_, hi = lo + stage_bytes_;
     const int which = parity_;

@@ -18,8 +18,8 @@
  * tile b / nseg of segment b % nseg, so the workgroups in flight read from every peer at once
  * and all xGMI links carry traffic together.  Remote segments (pushes into a peer's memory) may
  * share a launch with pulls: the pipelined allreduce sends one chunk out while it gathers an
- * older one in, over both directions of every link at once.  Tiles are 256 lanes x 16 B (kUnroll = 1: 4 KiB per
- * workgroup), like the other streaming kernels (kernels.hip).
+ * older one in, over both directions of every link at once.  Tiles are 256 lanes x 16 B
+ * (kUnroll = 1: 4 KiB per workgroup), like the other streaming kernels (kernels.hip).
  */
 #include <hip/hip_runtime.h>
 

@@ -6,7 +6,9 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -95,6 +97,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   }
   if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
   if (is("rabit_device_calibrate_test")) calibrate_test_ = utils::StringToBool(val);
+  if (is("rabit_device_calibration_adopt")) adopt_calibration_ = utils::StringToBool(val);
   if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
@@ -207,6 +210,41 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_trace_capacity")) trace_capacity_ = static_cast<size_t>(atol(val));
 }
 
+namespace {
+/*! \brief seconds since this process started (/proc/self/stat field 22 against /proc/uptime;
+ *  0 when unavailable): a restarted worker's start-up cost in the recovery breakdown */
+double ProcessAgeSeconds() {
+  FILE *f = fopen("/proc/self/stat", "r");
+  if (f == nullptr) return 0;
+  char buf[1024];
+  const size_t k = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[k] = '\0';
+  const char *p = strrchr(buf, ')');  // the command name may contain spaces
+  if (p == nullptr) return 0;
+  unsigned long long start = 0;
+  // fields after the name: state (3) ... starttime (22)
+  int field = 2;
+  for (const char *q = p + 1; *q != '\0'; ++q) {
+    if (*q == ' ') {
+      ++field;
+      if (field == 22) {
+        start = strtoull(q + 1, nullptr, 10);
+        break;
+      }
+    }
+  }
+  double up = 0;
+  f = fopen("/proc/uptime", "r");
+  if (f == nullptr) return 0;
+  if (fscanf(f, "%lf", &up) != 1) up = 0;
+  fclose(f);
+  const long hz = sysconf(_SC_CLK_TCK);
+  if (up <= 0 || hz <= 0 || start == 0) return 0;
+  return std::max(0.0, up - static_cast<double>(start) / static_cast<double>(hz));
+}
+}  // namespace
+
 bool EngineBase::Init(int argc, char *argv[]) {
   // before this engine starts any thread (watchdog, copier, bring-up helpers)
   device::DevicePlane::ConfigureRcclEnv();
@@ -255,6 +293,7 @@ bool EngineBase::Init(int argc, char *argv[]) {
     dev_.reset(new device::DevicePlane(dcfg_, rank_));
     if (user_stream_ != nullptr) dev_->SetUserStream(static_cast<hipStream_t>(user_stream_));
   }
+  stats_.t_process_start_to_init = ProcessAgeSeconds();
   return true;
 }
 
@@ -848,6 +887,22 @@ void EngineBase::LazyCheckPoint(const Serializable *) {
   stats_.n_checkpoint += 1;
 }
 
+std::string EngineBase::PhasesJson() const {
+  const EngineStats::Phases &p = stats_.phases;
+  std::ostringstream os;
+  os << "{\"detect\":" << p.detect << ",\"drop_links\":" << p.drop_links
+     << ",\"relink\":" << p.relink << ",\"records\":" << p.records
+     << ",\"peer_open\":" << p.peer_open << ",\"rccl\":" << p.rccl << ",\"tune\":" << p.tune
+     << ",\"calibration\":" << p.calibration << ",\"adopt\":" << p.adopt
+     << ",\"load_checkpoint\":" << p.load_checkpoint << ",\"replay\":" << p.replay
+     << ",\"serve_load\":" << p.serve_load << ",\"serve_replay\":" << p.serve_replay
+     << ",\"bringups\":" << p.bringups << ",\"calibrations\":" << p.calibrations
+     << ",\"adoptions\":" << p.adoptions << ",\"replays\":" << p.replays
+     << ",\"serves\":" << p.serves
+     << ",\"process_start_to_init\":" << stats_.t_process_start_to_init << "}";
+  return os.str();
+}
+
 std::string EngineBase::StatsJson() const {
   std::ostringstream os;
   const EngineStats &s = stats_;
@@ -858,6 +913,10 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
      << ",\"zero_copy_registry\":" << (dev_ ? dev_->RegistryJson() : std::string("{}"))
+     << ",\"recovery_phases_s\":" << PhasesJson()
+     << ",\"calib_matrix\":" << calib_matrix_json_
+     << ",\"rccl_init_refused\":" << (dev_ ? dev_->init_refused() : 0)
+     << ",\"rccl_live_abandoned\":" << device::DevicePlane::LiveAbandonedInits()
      << ",\"oneshot_ops\":" << (dev_ ? dev_->oneshot_ops() : 0)
      << ",\"fused_chunks\":" << (dev_ ? dev_->fused_chunks() : 0)
      << ",\"fused_oneshots\":" << (dev_ ? dev_->fused_oneshots() : 0)

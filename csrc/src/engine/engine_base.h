@@ -46,6 +46,24 @@ struct EngineStats {
   double bytes_allreduce{0}, bytes_broadcast{0}, bytes_allgather{0};
   double t_allreduce{0}, t_broadcast{0}, t_allgather{0}, t_checkpoint{0}, t_consensus{0};
   double t_recover{0};
+  /*!
+   * \brief where recovery time goes (seconds, summed over the job), survivor and restarted side:
+   *        detect: from the start of the failed op attempt to the failure seen; drop_links:
+   *        closing links and the reconnect stagger; relink: the tracker round; then the device
+   *        bring-up of the next epoch (records: GPU records over the host ring; peer_open:
+   *        preflight + IPC mapping of the direct transport; rccl: communicator bring-up; tune:
+   *        RCCL channel tuning; calibration: full start-up calibration; adopt: adopting the
+   *        survivors' calibration + one verified op per transport); load_checkpoint (the
+   *        restarted rank's LoadCheckPoint), replay (its result catch-up), serve_load /
+   *        serve_replay (survivors serving them)
+   */
+  struct Phases {
+    double detect{0}, drop_links{0}, relink{0};
+    double records{0}, peer_open{0}, rccl{0}, tune{0}, calibration{0}, adopt{0};
+    double load_checkpoint{0}, replay{0}, serve_load{0}, serve_replay{0};
+    uint64_t bringups{0}, calibrations{0}, adoptions{0}, replays{0}, serves{0};
+  } phases;
+  double t_process_start_to_init{0};  // this process: start to Init done (restart cost)
 };
 
 class EngineBase : public IEngine {
@@ -278,8 +296,8 @@ class EngineBase : public IEngine {
   int ckpt_mirror_mode_{0};          // rabit_device_ckpt_mirror: 0 idle, 1 always, 2 off
   int ckpt_slots_{0};                // rabit_device_ckpt_slots: 2, 3, 0 = by size
   bool mirror_low_prio_{false};      // rabit_device_mirror_priority=low
-  int mirror_ctas_{0};               // rabit_device_mirror_ctas: D2H mirror kernel width (> 0: kernel engine)
-  int mirror_engine_{-1};            // rabit_device_mirror_engine: hip / kernel / sdma (-1: by ctas)
+  int mirror_ctas_{0};     // rabit_device_mirror_ctas: D2H mirror kernel width (> 0: kernel)
+  int mirror_engine_{-1};  // rabit_device_mirror_engine: hip / kernel / sdma (-1: by ctas)
   size_t ckpt_3slot_max_{size_t(4) << 30};  // by size: 3 slots below this many bytes
   size_t shm_min_{1u << 20};        // rabit_host_shm_min
   size_t shm_stage_{32u << 20};     // rabit_host_shm_buffer (per stage, two per rank)
@@ -306,6 +324,22 @@ class EngineBase : public IEngine {
   static constexpr int kCalibForms = 5;
   double calib_form_us_[kCalibForms]{-1, -1, -1, -1, -1};
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
+  bool calib_valid_{false};     // this process holds a calibration of this job (adoptable)
+  std::string calib_matrix_json_{"{}"};  // the last calibration's times and bands (stats)
+  bool adopt_calibration_{true};  // rabit_device_calibration_adopt: recovery epochs adopt the
+                                  // survivors' calibration instead of re-measuring
+  /*! \brief collective: if some rank holds this job's calibration (a recovery epoch), every rank
+   *  takes the lowest such rank's routing and direct form, and one small op per transport is
+   *  verified on the host; *adopted false: calibrate from scratch */
+  Status AdoptCalibration(bool *adopted);
+  /*! \brief this rank's routing and calibration results, serialized (AdoptCalibration) */
+  std::string SerializeCalibration() const;
+  void ApplyCalibration(const std::string &blob);
+  /*! \brief one host-verified allreduce per transport of the routing (direct: 1 MiB, RCCL:
+   *  64 KiB); *good false on a wrong result, a non-success status on a failed op */
+  Status VerifyTransports(bool *good);
+  /*! \brief the recovery phase breakdown as JSON */
+  std::string PhasesJson() const;
   /*! \brief last broadcast calibration: rccl small/big, direct small/big (s; 0 = not run) */
   double calib_bcast_[4]{0, 0, 0, 0};
   bool mock_rccl_fail_{false};  // test hook: the RCCL communicator never comes up
@@ -313,7 +347,7 @@ class EngineBase : public IEngine {
   bool rccl_tune_{false};          // rabit_rccl_tune: time RCCL channel counts at start-up
   bool rccl_tuned_{false};         // this process took part in (or adopted) a tuning
   std::string rccl_tune_ctas_{"64,112"};  // candidate CTA counts besides RCCL's own choice
-  std::string rccl_tune_json_{"{}"};      // what the tuning measured (stats)          // epochs whose RCCL communicator did not come up on every rank
+  std::string rccl_tune_json_{"{}"};      // what the tuning measured (stats)
   bool dev_hang_armed_{false};     // set by the mock engine's mock_dev_hang
   bool die_mid_armed_{false};      // set by the mock engine's mock_die_mid
   double dev_hang_max_sec_{90};     // an injected hang ends by itself after this long

@@ -156,7 +156,8 @@ class EngineMock : public EngineRobust {
     }
     tsum_allreduce_ = tsum_allgather_ = 0.0;
   }
-  void CheckPointDevice(const Serializable *global_model, const Serializable *local_model) override {
+  void CheckPointDevice(const Serializable *global_model,
+                        const Serializable *local_model) override {
     Verify("CheckPoint");
     EngineRobust::CheckPointDevice(global_model, local_model);
   }

@@ -172,6 +172,10 @@ void EngineRobust::SetParam(const char *name, const char *val) {
   if (!strcmp(name, "rabit_global_replica")) num_global_replica_ = atoi(val);
   if (!strcmp(name, "rabit_local_replica")) num_local_replica_ = atoi(val);
   if (!strcmp(name, "rabit_elide_consensus")) elide_consensus_ = utils::StringToBool(val);
+  if (!strcmp(name, "rabit_recover_stagger_ms")) {
+    recover_stagger_ms_ = atof(val);
+    utils::Check(recover_stagger_ms_ >= 0, "rabit_recover_stagger_ms should be non negative");
+  }
   if (!strcmp(name, "rabit_hang_timeout_sec")) {
     hang_timeout_sec_ = atof(val);
     utils::Check(hang_timeout_sec_ >= 0, "rabit_hang_timeout_sec should be non negative");

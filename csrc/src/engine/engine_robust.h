@@ -57,7 +57,8 @@ class EngineRobust : public EngineBase {
                  const int _line, const char *_caller) override;
   void InitAfterException() override;
   int LoadCheckPoint(Serializable *global_model, Serializable *local_model) override;
-  void CheckPointDevice(const Serializable *global_model, const Serializable *local_model) override {
+  void CheckPointDevice(const Serializable *global_model,
+                        const Serializable *local_model) override {
     CheckPointImpl(global_model, local_model, true);
   }
   void CheckPoint(const Serializable *global_model, const Serializable *local_model) override {
@@ -291,6 +292,8 @@ class EngineRobust : public EngineBase {
   std::atomic<bool> watchdog_fired_{false};
   std::atomic<int> wd_rank_{-1};  // rank as seen by the watchdog thread (rank_ is not atomic)
   double hang_timeout_sec_{0};    // rabit_hang_timeout_sec (0: off)
+  double attempt_start_{0};       // start of the current op attempt (recovery phase "detect")
+  double recover_stagger_ms_{10}; // rabit_recover_stagger_ms: reconnect delay per rank
 };
 }  // namespace engine
 }  // namespace rabit

@@ -235,7 +235,9 @@ Status EngineRobust::TryRecoverLocalState(int v) {
       }
     }
     bool want = false;
-    for (const SlotCopy &c : plan) want = want || (c.r == rank_ && c.h != rank_ && Mod(c.r - c.k, n) == src);
+    for (const SlotCopy &c : plan) {
+      want = want || (c.r == rank_ && c.h != rank_ && Mod(c.r - c.k, n) == src);
+    }
     if (role != kHaveData && want) role = kRequestData;
     int recv_link;
     std::vector<bool> req_in;

@@ -84,8 +84,8 @@ void *LocalReplicas::Alloc(int v, int k, size_t bytes) {
       s.dev = nullptr;
     }
     // 2 MiB granules: steady checkpoints of a slowly growing state do not reallocate
-    const size_t cap = std::max<size_t>((bytes + (2u << 20) - 1) & ~static_cast<size_t>((2u << 20) - 1),
-                                        2u << 20);
+    const size_t granule = size_t(2) << 20;
+    const size_t cap = std::max<size_t>((bytes + granule - 1) & ~(granule - 1), granule);
     device::CheckHip(hipMalloc(&s.dev, cap), "hipMalloc(local slot)");
     s.cap = cap;
   }

@@ -39,6 +39,11 @@ bool EngineRobust::CheckAndRecover(Status s) {
   }
   const double t0 = utils::GetTime();
   trace::Scope ts("recover", rank_, version_number_, seq_counter_, 0, 0);
+  // detection: from the start of the attempt that failed to the failure seen here (the first
+  // failure of a recovery only: later ones are part of the recovery itself)
+  if (recovering_since_.load() == 0.0 && attempt_start_ > 0.0) {
+    stats_.phases.detect += t0 - attempt_start_;
+  }
   fast_mode_ = false;
   recover_counter_ += 1;
   stats_.n_recover_events += 1;
@@ -55,14 +60,21 @@ bool EngineRobust::CheckAndRecover(Status s) {
   ResetShm();
   // simplest consistent repair: drop every link so the failure propagates, then rejoin
   for (auto &l : topo_.links) l->sock.Close();
-  // spread the reconnect load on the tracker
+  // spread the reconnect load on the tracker (reference: 10 ms x rank; rabit_recover_stagger_ms)
   {
     core::WaitScope waiting;
-    std::this_thread::sleep_for(std::chrono::milliseconds(10 * std::max(rank_, 0)));
+    std::this_thread::sleep_for(
+        std::chrono::microseconds(static_cast<int64_t>(recover_stagger_ms_ * 1000.0) *
+                                  std::max(rank_, 0)));
   }
+  const double t1 = utils::GetTime();
+  stats_.phases.drop_links += t1 - t0;
   ReconnectLinks("recover");
   wd_rank_.store(rank_);
-  stats_.t_recover += utils::GetTime() - t0;
+  const double t2 = utils::GetTime();
+  stats_.phases.relink += t2 - t1;
+  attempt_start_ = t2;  // the next attempt (a failure of it is detected relative to this)
+  stats_.t_recover += t2 - t0;
   return false;
 }
 
@@ -307,6 +319,17 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
     return TryRecoverLocalState(!local_chkpt_version_);
   }
   trace::Scope ts("replay", rank_, version_number_, seqno, size, 0);
+  // time of this catch-up step: the requester's replay or a holder's / relay's serving
+  struct PhaseTimer {
+    double *acc;
+    double t0;
+    ~PhaseTimer() { *acc += utils::GetTime() - t0; }
+  } phase_timer{requester ? &stats_.phases.replay : &stats_.phases.serve_replay, utils::GetTime()};
+  if (requester) {
+    stats_.phases.replays += 1;
+  } else {
+    stats_.phases.serves += 1;
+  }
   RecoverType role;
   void *data = nullptr;
   bool data_dev = false;
@@ -417,6 +440,12 @@ Status EngineRobust::TryGetResult(void *sendrecvbuf, size_t size, int seqno, boo
 Status EngineRobust::TryLoadCheckPoint(bool requester) {
   const RecoverType role = requester ? kRequestData : kHaveData;
   Status s;
+  struct PhaseTimer {
+    double *acc;
+    double t0;
+    ~PhaseTimer() { *acc += utils::GetTime() - t0; }
+  } phase_timer{requester ? &stats_.phases.load_checkpoint : &stats_.phases.serve_load,
+                utils::GetTime()};
   if (num_local_replica_ != 0) {
     if (requester) local_.Clear(local_chkpt_version_);
     s = TryRecoverLocalState(local_chkpt_version_);
@@ -602,6 +631,7 @@ bool EngineRobust::RecoverExec(void *buf, size_t size, int flag, int seqno, int 
   }
   utils::Assert(seqno >= 0, "%s: negative seqno %d (flag %d, version %d)", caller, seqno, flag,
                 version_number_);
+  if (recovering_since_.load() == 0.0) attempt_start_ = utils::GetTime();
   // steady state: everybody agreed to execute the previous op and nobody saw a failure
   // since, so the only possible outcome of this round is "execute"
   if (fast_mode_ && flag == 0 && static_cast<uint32_t>(seqno) < ActionSummary::kLocalCheckPoint) {

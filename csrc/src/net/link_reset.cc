@@ -14,7 +14,9 @@ namespace net {
 namespace {
 enum Step : int { kSendUrgent, kSendMark, kDrain, kReadMark, kSendAck, kReadAck, kDone, kFailed };
 
-bool WouldBlock(ssize_t n) { return n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR); }
+bool WouldBlock(ssize_t n) {
+  return n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR);
+}
 }  // namespace
 
 Status ResetLinks(const std::vector<TcpSocket *> &socks, int timeout_ms) {

@@ -21,7 +21,8 @@
 namespace rabit {
 namespace net {
 
-/*! \brief outcome of a non-blocking transfer step (reference ReturnType, allreduce_base.h:257-296) */
+/*! \brief outcome of a non-blocking transfer step (reference ReturnType,
+ *  allreduce_base.h:257-296) */
 enum class Status : int {
   kSuccess = 0,
   kConnReset = 1,   // peer reset the connection
@@ -108,7 +109,8 @@ class Poller {
   void WatchRead(int fd) { Entry(fd).events |= POLLIN; }
   void WatchWrite(int fd) { Entry(fd).events |= POLLOUT; }
   void WatchHangup(int fd) { Entry(fd).events |= POLLRDHUP; }
-  /*! \brief urgent (out-of-band) data, e.g. a link-reset mark (reference PollHelper::WatchException) */
+  /*! \brief urgent (out-of-band) data, e.g. a link-reset mark
+   *  (reference PollHelper::WatchException) */
   void WatchExcept(int fd) { Entry(fd).events |= POLLPRI; }
   /*! \brief poll with a timeout in ms (-1 = infinite); returns poll()'s result */
   int Poll(int timeout_ms);

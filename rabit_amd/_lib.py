@@ -69,7 +69,8 @@ def build_info(lib: str = "standard") -> dict:
 
 
 def _declare(d: ctypes.CDLL) -> None:
-    c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
+    c_int, c_size_t = ctypes.c_int, ctypes.c_size_t
+    c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
     c_ulong, c_double = ctypes.c_ulong, ctypes.c_double
     prep_t = ctypes.CFUNCTYPE(None, c_void_p)
     sig = {

@@ -83,7 +83,8 @@ class HistGBDT:
             GL, HL = cum[..., 0], cum[..., 1]
             Gt, Ht = cum[:, 0, -1, 0], cum[:, 0, -1, 1]
             GR, HR = Gt[:, None, None] - GL, Ht[:, None, None] - HL
-            gain = GL ** 2 / (HL + lam) + GR ** 2 / (HR + lam) - (Gt ** 2 / (Ht + lam))[:, None, None]
+            parent = (Gt ** 2 / (Ht + lam))[:, None, None]
+            gain = GL ** 2 / (HL + lam) + GR ** 2 / (HR + lam) - parent
             ok = (HL >= self.mcw) & (HR >= self.mcw)
             ok[..., nb - 1] = False
             gain = torch.where(ok, gain, torch.full_like(gain, -1.0))

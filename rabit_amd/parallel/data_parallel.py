@@ -186,4 +186,5 @@ def shard(n: int, rank: int, world: int):
 
 def global_mean(x: np.ndarray) -> np.ndarray:
     """Mean over ranks (host arrays)."""
-    return rabit.allreduce(np.asarray(x, dtype=np.float64).copy(), rabit.SUM) / rabit.get_world_size()
+    total = rabit.allreduce(np.asarray(x, dtype=np.float64).copy(), rabit.SUM)
+    return total / rabit.get_world_size()

@@ -394,6 +394,57 @@ TEST(calibration_routing) {
   EXPECT(r.min_bytes == 0);
 }
 
+// the piecewise routing over several calibration points (routing.h: ChooseRoutes)
+TEST(calibration_routing_piecewise) {
+  using rabit::engine::ChooseRoutes;
+  using rabit::engine::RouteFor;
+  const double K = 1024, M = 1024 * 1024;
+  const std::vector<double> x = {64 * K, 1 * M, 4 * M, 32 * M, 128 * M};
+  // candidate 0 ("RCCL"): 30 us floor, 200 GB/s; candidate 1 ("direct"): 15 us, 150 GB/s; so
+  // direct below the crossover (~2.4 MB), RCCL above
+  auto lin = [](double a, double gbps, double s) { return a + s / (gbps * 1e9); };
+  std::vector<std::vector<double>> t(2, std::vector<double>(x.size()));
+  for (size_t i = 0; i < x.size(); ++i) {
+    t[0][i] = lin(30e-6, 200, x[i]);
+    t[1][i] = lin(15e-6, 150, x[i]);
+  }
+  auto r = ChooseRoutes(x, t);
+  EXPECT(r.size() == 2 && r[0].lo == 0 && r[0].choice == 1 && r[1].choice == 0);
+  const double cross = 15e-6 / (1 / 150e9 - 1 / 200e9);  // equal times there
+  EXPECT(std::abs(r[1].lo - cross) < 1.0);
+  EXPECT(RouteFor(r, 64 * K) == 1 && RouteFor(r, 128 * M) == 0 && RouteFor(r, 1e12) == 0);
+  // three candidates, two crossovers: 0 wins small, 1 in the middle (4-32 MiB), 2 large
+  std::vector<std::vector<double>> u = {{10e-6, 40e-6, 120e-6, 800e-6, 3000e-6},
+                                        {20e-6, 45e-6, 100e-6, 600e-6, 2600e-6},
+                                        {40e-6, 70e-6, 130e-6, 650e-6, 2000e-6}};
+  r = ChooseRoutes(x, u);
+  EXPECT(r.size() == 3 && r[0].choice == 0 && r[1].choice == 1 && r[2].choice == 2);
+  EXPECT(r[1].lo > 1 * M && r[1].lo < 4 * M && r[2].lo > 32 * M && r[2].lo < 128 * M);
+  // every measured point routes to its own fastest candidate
+  for (size_t i = 0; i < x.size(); ++i) {
+    int best = 0;
+    for (int c = 1; c < 3; ++c) best = u[c][i] < u[best][i] ? c : best;
+    EXPECT(RouteFor(r, x[i]) == best);
+  }
+  // a candidate that failed (< 0 everywhere) is never chosen; one measured only at some points
+  // competes only between them
+  u[0] = {-1, -1, -1, -1, -1};
+  r = ChooseRoutes(x, u);
+  EXPECT(RouteFor(r, 64 * K) == 1 && RouteFor(r, 128 * M) == 2);
+  u[1] = {5e-6, 6e-6, -1, -1, -1};
+  r = ChooseRoutes(x, u);
+  EXPECT(RouteFor(r, 64 * K) == 1 && RouteFor(r, 512 * K) == 1 && RouteFor(r, 8 * M) == 2);
+  // past the last point the last interval's lines extend: a flatter candidate takes over
+  std::vector<std::vector<double>> v = {{10e-6, 20e-6, 30e-6, 100e-6, 400e-6},
+                                        {50e-6, 55e-6, 60e-6, 120e-6, 410e-6}};
+  r = ChooseRoutes(x, v);
+  EXPECT(RouteFor(r, 128 * M) == 0 && RouteFor(r, 1024 * M) == 1);
+  // one point: one band; no measurement: no bands
+  EXPECT(ChooseRoutes({64 * K}, {{3e-6}, {2e-6}}).size() == 1);
+  EXPECT(ChooseRoutes({64 * K}, {{3e-6}, {2e-6}})[0].choice == 1);
+  EXPECT(ChooseRoutes({64 * K, 1 * M}, {{-1, -1}}).empty());
+}
+
 TEST(wait_state_working_vs_waiting) {
   using rabit::core::OpScope;
   using rabit::core::WaitScope;

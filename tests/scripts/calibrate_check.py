@@ -47,6 +47,22 @@ else:
     assert forms[1] == -1 and forms[3] == -1 and st["direct_fused"] == 0, (forms, st)
 fused = rabit.allreduce(np.array([st["direct_fused"]]), rabit.SUM)[0]
 assert fused in (0, world), fused
+# the piecewise calibration: every candidate at 5 sizes (64 KiB .. 128 MiB), size bands for the
+# transport and the direct form, the same on every rank; every measured point routes to its own
+# fastest form
+cm = st["calib_matrix"]
+assert cm["bytes"] == [64 << 10, 1 << 20, 4 << 20, 32 << 20, 128 << 20], cm
+assert len(cm["us"]["rccl"]) == 5 and all(v > 0 for v in cm["us"]["pull-classic"]), cm
+assert cm["transport_bands"] and cm["form_bands"] and cm["form_bands"][0]["from"] == 0, cm
+import json, zlib  # noqa: E401
+h = zlib.crc32(json.dumps(cm["form_bands"], sort_keys=True).encode()) & 0x7fffffff
+assert rabit.allreduce(np.array([h]), rabit.MIN)[0] == rabit.allreduce(np.array([h]), rabit.MAX)[0]
+for i, nb in enumerate(cm["bytes"]):
+    band = [b for b in cm["form_bands"] if b["from"] <= nb][-1]["form"]
+    times = {k: v[i] for k, v in cm["us"].items() if k != "rccl" and v[i] > 0}
+    assert band == min(times, key=times.get), (nb, band, times)
+ph = st["recovery_phases_s"]
+assert ph["bringups"] == 1 and ph["calibrations"] == 1 and ph["adoptions"] == 0, ph
 # with a symmetric heap that has room, the calibration reads its inputs from the heap's tail
 want_heap = any(a.startswith("rabit_device_symmetric_heap=") for a in sys.argv[1:])
 assert st["calib_heap_src"] == (1 if want_heap else 0), st

@@ -1,7 +1,6 @@
 """Device (HBM) checkpoints under failure: the model lives in HBM, checkpoints are HBM
 snapshots + pinned mirrors; a killed worker reloads its model from a survivor's lazy
 snapshot.  Collectives use host arrays (TCP), so several workers can share one GPU."""
-import os
 import sys
 
 import numpy as np

@@ -2,7 +2,6 @@
 transport usable (an allreduce after it is exact), and a second probe works too."""
 import sys
 
-import numpy as np
 import torch
 
 import rabit_amd as rabit

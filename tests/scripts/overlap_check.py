@@ -7,7 +7,6 @@ Prints the final-weight digest (identical on every rank and, for the same job, i
 and the median step time.  Workers killed by mock kill points resume from the last checkpoint.
 """
 import hashlib
-import os
 import sys
 import time
 

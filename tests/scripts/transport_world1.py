@@ -6,7 +6,6 @@ and gather kernels.  At world 1 every result equals the input.  argv[1]: rccl | 
 import ctypes
 import sys
 
-import numpy as np
 import torch
 
 import rabit_amd as rabit

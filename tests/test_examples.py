@@ -6,7 +6,6 @@ import os
 import re
 import sys
 
-import pytest
 
 from rabit_amd.launcher import LocalJob
 

@@ -2,7 +2,6 @@
 several ranks sharing the GPU through the direct transport, with a worker killed mid-way."""
 import os
 import subprocess
-import sys
 
 import pytest
 

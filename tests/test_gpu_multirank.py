@@ -159,6 +159,16 @@ def test_host_stage_auto_across_restart(mock):
     assert "resumed at version" in out, out[-3000:]
 
 
+def test_recovery_epoch_adopts_calibration():
+    """after a kill, the next device epoch takes the survivors' calibration (one verified op per
+    transport) instead of re-measuring it, on the restarted rank as on the survivors"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("calib_adopt_check.py", 3, ["mock=1,1,0,0"], attempts=3)
+    assert rc == 0, out[-5000:]
+    assert out.count("CALIBADOPT OK") == 3, out[-3000:]
+
+
 @pytest.mark.parametrize("extra", [[], ["rabit_device_symmetric_heap=160M"],
                                    ["rabit_device_fused=auto"]])
 def test_calibration_flow(extra):

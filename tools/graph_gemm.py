@@ -1,7 +1,6 @@
 """Does a captured GEMM replay exactly?  Capture C = A @ B (and A^T/B^T forms) in a hipGraph,
 replay it several times and compare every replay with the eager product."""
 import json
-import sys
 
 import torch
 

@@ -4,7 +4,6 @@ import json
 import sys
 import time
 
-import numpy as np
 import torch
 
 import rabit_amd as rabit
