@@ -1218,6 +1218,14 @@ Status DevicePlane::Exchange(const std::vector<ExchangeItem> &plan, size_t *byte
   return RunP2P(ops, at, "exchange", probe);
 }
 
+Status DevicePlane::AllgatherResolved(void *buf, size_t total, size_t begin, size_t size,
+                                      void *log) {
+  utils::Check(peers_ != nullptr && UseDirect(total), "resolved allgather needs the direct path");
+  op_bytes_ = total;
+  CheckHip(peers_->AllgatherResolved(buf, total, begin, size, log), "direct allgather");
+  return Status::kSuccess;
+}
+
 Status DevicePlane::AllgatherV(void *buf_, size_t total, const std::vector<size_t> &begin,
                                const std::vector<size_t> &size, const FailureProbe &probe,
                                void *log) {

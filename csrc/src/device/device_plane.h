@@ -439,6 +439,14 @@ class DevicePlane {
   Status AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                     const std::vector<size_t> &size, const FailureProbe &probe,
                     void *log = nullptr);
+  /*! \brief true when an allgather of this size needs every rank's slice on the host first
+   *  (RCCL's grouped broadcasts); the direct transport resolves the layout on the device */
+  bool AllgatherNeedsLayout(size_t total) const { return !UseDirect(total); }
+  /*! \brief rabit Allgather knowing only this rank's slice (direct transport only: see
+   *  AllgatherNeedsLayout) */
+  Status AllgatherResolved(void *buf, size_t total, size_t begin, size_t size,
+                           void *log = nullptr);
+  uint64_t resolved_allgathers() const { return peers_ ? peers_->resolved_allgathers() : 0; }
   /*!
    * \brief point-to-point copies over xGMI (see ExchangeItem; every rank passes the same plan).
    *        With RCCL: one grouped ncclSend/ncclRecv call on the ranks that take part (the others

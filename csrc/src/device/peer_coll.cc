@@ -109,6 +109,9 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
   void *tbl = nullptr;
   CheckHip(hipMalloc(&tbl, kMaxPeers * sizeof(void *)), "hipMalloc(source table)");
   table_ = static_cast<const void **>(tbl);
+  void *mt = nullptr;
+  CheckHip(hipMalloc(&mt, 2 * kMaxPeers * sizeof(unsigned long long)), "hipMalloc(meta table)");
+  meta_table_ = static_cast<unsigned long long *>(mt);
   void *hw = nullptr;
   CheckHip(hipHostMalloc(&hw, 64, hipHostMallocCoherent | hipHostMallocMapped),
            "hipHostMalloc(peer words)");
@@ -135,6 +138,7 @@ PeerGroup::~PeerGroup() {
     }
   }
   if (table_ != nullptr) (void)hipFree(const_cast<void **>(table_));
+  if (meta_table_ != nullptr) (void)hipFree(meta_table_);
   if (base_ != nullptr) (void)hipFree(base_);
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
 }
@@ -885,6 +889,56 @@ hipError_t PeerGroup::AllgatherV(void *buf, size_t total, const std::vector<size
   }
   return hipSuccess;
 }
+hipError_t PeerGroup::AllgatherResolved(void *buf, size_t total, size_t begin, size_t size,
+                                        void *log) {
+  utils::Assert(opened_, "peer group not opened");
+  done_pending_ = false;
+  if (total == 0) return hipSuccess;
+  char *user = static_cast<char *>(buf);
+  char *lg = static_cast<char *>(log);
+  begin %= total;
+  size_t lo[2], hi[2];
+  const int k = SliceRanges(begin, size, total, lo, hi);
+  for (size_t wlo = 0; wlo < total; wlo += stage_bytes_) {
+    const size_t whi = std::min(total, wlo + stage_bytes_);
+    const int which = parity_;
+    parity_ ^= 1;
+    // own slice's part of the window into the stage (and the log slot, dual store)
+    CopyBatch b;
+    NewBatch(&b);
+    for (int j = 0; j < k; ++j) {
+      const size_t a = std::max(lo[j], wlo), z = std::min(hi[j], whi);
+      if (z > a) {
+        AddSeg(&b, stage(rank_, which) + (a - wlo), user + a, lg != nullptr ? lg + a : nullptr,
+               z - a);
+      }
+    }
+    if (b.n > 0) XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    // the barrier publishes this rank's slice and resolves everybody's into the meta table
+    ResolveArgs ra{};
+    ra.parity = which;
+    ra.table = nullptr;
+    ra.my_meta[0] = static_cast<unsigned long long>(begin);
+    ra.my_meta[1] = static_cast<unsigned long long>(size);
+    ra.meta_table = meta_table_;
+    XRABIT_TRY_HIP(Barrier(&ra));
+    AllgatherWindowArgs ga{};
+    for (int p = 0; p < n_; ++p) ga.stage[p] = stage(p, which);
+    ga.meta_table = meta_table_;
+    ga.buf = user;
+    ga.log = lg;
+    ga.total = total;
+    ga.wlo = wlo;
+    ga.whi = whi;
+    ga.n = n_;
+    ga.rank = rank_;
+    ga.guard = dev_status();
+    XRABIT_TRY_HIP(LaunchAllgatherWindow(ga, stream_));
+  }
+  ++resolved_allgathers_;
+  return hipSuccess;
+}
+
 hipError_t PeerGroup::Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in) {
   utils::Assert(opened_, "peer group not opened");
   done_pending_ = false;

@@ -55,6 +55,10 @@ constexpr size_t kPeerStatusOffset = 4096;
 /*! \brief two mailbox words (by stage parity): where this rank's input of the current chunk
  *  lives, published before the first barrier of the chunk (see ResolveArgs) */
 constexpr size_t kPeerMailboxOffset = 8192;
+/*! \brief per parity, this rank's (begin, size) slice of the current allgather window, published
+ *  by the window's barrier (ResolveArgs::meta_table): peers resolve the whole slice layout on the
+ *  device, so no host round exchanges it (PeerGroup::AllgatherResolved) */
+constexpr size_t kPeerMetaOffset = kPeerMailboxOffset + 64;
 /*! \brief mailbox flag: the offset is into the symmetric heap, not the stage allocation */
 constexpr unsigned long long kMailboxHeap = 1ull << 63;
 
@@ -94,7 +98,27 @@ struct ResolveArgs {
   const void **table;               // out: n source pointers
   // registered allocations (peer_registry.h): [peer][slot] mapped bases, for kMailboxReg words
   const char *const *reg_table;
+  // optional allgather slice layout: publish my_meta (begin, size) before signalling, and after
+  // the wait copy every rank's pair into meta_table[2 p .. 2 p + 1] (device memory)
+  unsigned long long my_meta[2];
+  unsigned long long *meta_table;
 };
+
+/*!
+ * \brief the gather of one allgather window whose slice layout lives on the device (meta_table,
+ *        filled by the window's barrier): every byte of [wlo, whi) that belongs to another rank's
+ *        slice (slices partition [0, total) and may wrap) is copied from that rank's stage (at
+ *        offset - wlo) into buf, and into log when given
+ */
+struct AllgatherWindowArgs {
+  const char *stage[kMaxPeers];            // stage of this window's parity, per rank (mapped)
+  const unsigned long long *meta_table;    // 2 n words: (begin, size) per rank
+  char *buf, *log;
+  size_t total, wlo, whi;
+  int n, rank;
+  const int *guard;                        // the group's failure word
+};
+hipError_t LaunchAllgatherWindow(const AllgatherWindowArgs &args, hipStream_t stream);
 
 /*!
  * \brief the fused two-shot allreduce of one chunk (fused_allreduce.hip): ONE launch replaces
@@ -246,6 +270,14 @@ class PeerGroup {
   uint64_t bcast_chunks() const { return bcast_chunks_; }
   hipError_t AllgatherV(void *buf, size_t total, const std::vector<size_t> &begin,
                         const std::vector<size_t> &size, void *log = nullptr);
+  /*!
+   * \brief rabit's allgather knowing only this rank's slice [begin, begin + size) mod total:
+   *        every window's barrier publishes the slice and resolves everybody's on the device,
+   *        and the gather kernel finds each byte's owner there (no host metadata round)
+   */
+  hipError_t AllgatherResolved(void *buf, size_t total, size_t begin, size_t size,
+                               void *log = nullptr);
+  uint64_t resolved_allgathers() const { return resolved_allgathers_; }
   /*!
    * \brief point-to-point copies between ranks (a collective: every rank passes the same plan).
    *        Each sender streams the distinct payloads it owns through its stage buffer, one
@@ -465,6 +497,8 @@ class PeerGroup {
   bool done_signal_{true};
   size_t bcast_chunk_{0};
   uint64_t bcast_ops_{0}, bcast_chunks_{0};
+  uint64_t resolved_allgathers_{0};
+  unsigned long long *meta_table_{nullptr};  // device: 2 kMaxPeers words
   bool done_pending_{false};
   unsigned long long done_epoch_{0};
 };

@@ -60,12 +60,26 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
                                                   kPeerMailboxOffset) +
            resolve.parity;
   };
+  // the allgather slice layout (begin, size) of this window, by parity like the mailbox
+  auto meta = [&](int p) {
+    return reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(flags.p[p]) +
+                                                  kPeerMetaOffset) +
+           2 * resolve.parity;
+  };
   if (RESOLVE) {
     if (t == 0) {
-      __hip_atomic_store(mailbox(rank), resolve.my_mailbox, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      if (resolve.table != nullptr) {
+        __hip_atomic_store(mailbox(rank), resolve.my_mailbox, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (resolve.meta_table != nullptr) {
+        __hip_atomic_store(meta(rank), resolve.my_meta[0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(meta(rank) + 1, resolve.my_meta[1], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
-    __syncthreads();  // the mailbox store precedes every lane's flag store below
+    __syncthreads();  // the mailbox / meta stores precede every lane's flag store below
   }
   // make the bytes written by earlier kernels of this stream visible before signalling
   __threadfence_system();
@@ -85,7 +99,15 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
   __threadfence_system();
   if (RESOLVE) {
     __syncthreads();
-    if (t < n && __hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+    if (t < n && resolve.meta_table != nullptr &&
+        __hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+      resolve.meta_table[2 * t] =
+          __hip_atomic_load(meta(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      resolve.meta_table[2 * t + 1] =
+          __hip_atomic_load(meta(t) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (t < n && resolve.table != nullptr &&
+        __hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
       const unsigned long long m =
           __hip_atomic_load(mailbox(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const char *src;
@@ -211,7 +233,77 @@ __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
     }
   }
 }
+/*! \brief a workgroup copies [0, bytes) of src to dst (and dst2): 16-byte vectors when the three
+ *  share their alignment modulo 16 (head and tail bytes apart), bytes otherwise */
+__device__ __forceinline__ void BlockCopy(char *dst, const char *src, char *dst2, size_t bytes) {
+  const uintptr_t md = reinterpret_cast<uintptr_t>(dst) & 15u;
+  const uintptr_t ms = reinterpret_cast<uintptr_t>(src) & 15u;
+  const uintptr_t m2 = dst2 != nullptr ? reinterpret_cast<uintptr_t>(dst2) & 15u : md;
+  size_t head = bytes, nv = 0;
+  if (md == ms && m2 == md) {
+    head = md != 0 ? std::min<size_t>(bytes, 16 - md) : 0;
+    nv = (bytes - head) / 16;
+  }
+  for (size_t i = threadIdx.x; i < head; i += kBlock) {
+    dst[i] = src[i];
+    if (dst2 != nullptr) dst2[i] = src[i];
+  }
+  const uint4 *s4 = reinterpret_cast<const uint4 *>(src + head);
+  uint4 *d4 = reinterpret_cast<uint4 *>(dst + head);
+  uint4 *e4 = dst2 != nullptr ? reinterpret_cast<uint4 *>(dst2 + head) : nullptr;
+  for (size_t i = threadIdx.x; i < nv; i += kBlock) {
+    const uint4 v = s4[i];
+    d4[i] = v;
+    if (e4 != nullptr) e4[i] = v;
+  }
+  for (size_t i = head + nv * 16 + threadIdx.x; i < bytes; i += kBlock) {
+    dst[i] = src[i];
+    if (dst2 != nullptr) dst2[i] = src[i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void AllgatherWindowKernel(AllgatherWindowArgs a) {
+  if (a.guard != nullptr &&
+      __hip_atomic_load(a.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    return;
+  }
+  __shared__ unsigned long long s_meta[2 * kMaxPeers];
+  if (threadIdx.x < 2 * a.n) s_meta[threadIdx.x] = a.meta_table[threadIdx.x];
+  __syncthreads();
+  const size_t tlo = a.wlo + static_cast<size_t>(blockIdx.x) * kTileBytes;
+  if (tlo >= a.whi) return;
+  const size_t thi = std::min(a.whi, tlo + kTileBytes);
+  for (int p = 0; p < a.n; ++p) {
+    if (p == a.rank) continue;
+    const size_t size = static_cast<size_t>(s_meta[2 * p + 1]);
+    if (size == 0 || a.total == 0) continue;
+    const size_t begin = static_cast<size_t>(s_meta[2 * p]) % a.total;
+    // the slice [begin, begin + size) mod total: at most two ranges
+    size_t lo[2] = {begin, 0}, hi[2] = {std::min(a.total, begin + size), 0};
+    const int k = begin + size > a.total ? 2 : 1;
+    if (k == 2) hi[1] = begin + size - a.total;
+    for (int j = 0; j < k; ++j) {
+      const size_t x0 = std::max(lo[j], tlo), x1 = std::min(hi[j], thi);
+      if (x1 <= x0) continue;
+      BlockCopy(a.buf + x0, a.stage[p] + (x0 - a.wlo), a.log != nullptr ? a.log + x0 : nullptr,
+                x1 - x0);
+    }
+  }
+}
 }  // namespace
+
+hipError_t LaunchAllgatherWindow(const AllgatherWindowArgs &args, hipStream_t stream) {
+  if (args.n < 1 || args.n > kMaxPeers || args.rank < 0 || args.rank >= args.n ||
+      args.whi < args.wlo || args.meta_table == nullptr) {
+    return hipErrorInvalidValue;
+  }
+  const size_t tiles = (args.whi - args.wlo + kTileBytes - 1) / kTileBytes;
+  if (tiles == 0) return hipSuccess;
+  if (tiles > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(AllgatherWindowKernel, dim3(static_cast<unsigned>(tiles)), dim3(kBlock), 0,
+                     stream, args);
+  return hipGetLastError();
+}
 
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n,
                              unsigned long long *counter, const volatile int *abort_word,

@@ -98,6 +98,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_device_calibrate")) calibrate_ = utils::StringToBool(val);
   if (is("rabit_device_calibrate_test")) calibrate_test_ = utils::StringToBool(val);
   if (is("rabit_device_calibration_adopt")) adopt_calibration_ = utils::StringToBool(val);
+  if (is("rabit_device_allgather_resolve")) allgather_resolve_ = utils::StringToBool(val);
   if (is("rabit_device_replay")) device_replay_ = utils::StringToBool(val);
   if (is("rabit_host_via_device")) host_via_device_ = utils::StringToBool(val);
   if (is("rabit_host_via_device_min")) host_dev_min_ = core::ParseUnit(name, val);
@@ -612,20 +613,30 @@ Status EngineBase::TryAllgather(void *buf, size_t total, size_t begin, size_t en
     }
     return Status::kSuccess;
   }
-  // every rank needs every slice: exchange (begin, size) pairs over the host ring first
+  Status s = EnsureDeviceComm();
+  if (s != Status::kSuccess) return s;
+  if (allgather_resolve_ && !dev_->AllgatherNeedsLayout(total)) {
+    // the direct transport: every window's barrier publishes this rank's slice and the gather
+    // kernel resolves the owners on the device -- no host round before the op
+    stats_.n_device_ops += 1;
+    dev_->EnterFromUser();
+    MaybeInjectDeviceHang();
+    s = dev_->AllgatherResolved(buf, total, begin, end - begin, dev_log);
+    if (s != Status::kSuccess) return s;
+    return dev_->Finish(MakeProbe());
+  }
+  // RCCL's grouped broadcasts need every rank's slice: exchange (begin, size) over the host ring
   const int n = GetWorldSize();
   std::vector<uint64_t> meta(2 * n, 0);
   meta[2 * rank_] = begin;
   meta[2 * rank_ + 1] = end - begin;
-  Status s = host_->RingAllgather(meta.data(), meta.size() * 8, 16 * rank_, 16 * rank_ + 16, 16);
+  s = host_->RingAllgather(meta.data(), meta.size() * 8, 16 * rank_, 16 * rank_ + 16, 16);
   if (s != Status::kSuccess) return s;
   std::vector<size_t> b(n), z(n);
   for (int r = 0; r < n; ++r) {
     b[r] = static_cast<size_t>(meta[2 * r]);
     z[r] = static_cast<size_t>(meta[2 * r + 1]);
   }
-  s = EnsureDeviceComm();
-  if (s != Status::kSuccess) return s;
   stats_.n_device_ops += 1;
   dev_->EnterFromUser();
   MaybeInjectDeviceHang();
@@ -913,6 +924,7 @@ std::string EngineBase::StatsJson() const {
      << ",\"device_direct\":" << (dev_ && dev_->has_peers() ? 1 : 0)
      << ",\"zero_copy_chunks\":" << (dev_ ? dev_->zero_copy_chunks() : 0)
      << ",\"zero_copy_registry\":" << (dev_ ? dev_->RegistryJson() : std::string("{}"))
+     << ",\"resolved_allgathers\":" << (dev_ ? dev_->resolved_allgathers() : 0)
      << ",\"recovery_phases_s\":" << PhasesJson()
      << ",\"calib_matrix\":" << calib_matrix_json_
      << ",\"rccl_init_refused\":" << (dev_ ? dev_->init_refused() : 0)

@@ -326,6 +326,8 @@ class EngineBase : public IEngine {
   bool calib_heap_src_{false};  // the last calibration read its inputs from the symmetric heap
   bool calib_valid_{false};     // this process holds a calibration of this job (adoptable)
   std::string calib_matrix_json_{"{}"};  // the last calibration's times and bands (stats)
+  bool allgather_resolve_{true};  // rabit_device_allgather_resolve: direct allgathers resolve
+                                  // the slice layout on the device (0: a host round first)
   bool adopt_calibration_{true};  // rabit_device_calibration_adopt: recovery epochs adopt the
                                   // survivors' calibration instead of re-measuring
   /*! \brief collective: if some rank holds this job's calibration (a recovery epoch), every rank

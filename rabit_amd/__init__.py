@@ -8,8 +8,9 @@
 See core.py for the API, tracker.py / launcher.py for job launch.
 """
 from .core import (BITOR, DTYPE_ENUM, DTYPE_ENUM__, MAX, MIN, PREP_ABS, PREP_COPY,  # noqa: F401
-                   PREP_SCALE, PREP_SQUARE, SUM, allgather, allreduce, allreduce_prepared,
-                   broadcast, broadcast_tensor, checkpoint, engine_name, finalize, get_device,
+                   PREP_SCALE, PREP_SQUARE, SUM, allgather, allgather_slice, allreduce,
+                   allreduce_prepared, broadcast, broadcast_tensor, checkpoint, engine_name,
+                   finalize, get_device,
                    get_processor_name, get_rank, get_ring_prev_rank, get_world_size, init,
                    is_distributed, last_error, lazy_checkpoint, lib, load_checkpoint,
                    set_error_mode, stats, tracker_print, version_number, dump_trace,

@@ -298,6 +298,29 @@ def allgather(data):
     return out
 
 
+def allgather_slice(data, begin: int, size: int, size_prev_slice: int = 0):
+    """rabit's general Allgather, in place: this rank owns data[begin : begin + size] (element
+    indices, wrapping modulo len(data)); afterwards data holds every rank's slice.  The slices
+    of all ranks partition data, ring-ordered: the next rank's slice starts where this one ends
+    (reference `include/rabit/rabit.h` Allgather).  A contiguous torch tensor (HBM or host) or
+    numpy array; returned.  size_prev_slice: the previous rank's slice size (the host ring uses
+    it; the device transports do not need it)."""
+    _check_init()
+    if _is_torch(data):
+        if not data.is_contiguous():
+            raise ValueError("allgather_slice needs a contiguous tensor")
+        if data.is_cuda:
+            _sync_stream_for(data)
+        _LIB.RabitAllgather(ctypes.c_void_p(data.data_ptr()), data.numel(), int(begin),
+                            int(size), int(size_prev_slice), _torch_dtype_enum(data))
+        return data
+    if not (isinstance(data, np.ndarray) and data.flags.c_contiguous):
+        raise TypeError("allgather_slice takes a contiguous numpy array or torch tensor")
+    _LIB.RabitAllgather(data.ctypes.data_as(ctypes.c_void_p), data.size, int(begin), int(size),
+                        int(size_prev_slice), DTYPE_ENUM[data.dtype])
+    return data
+
+
 def _load_model(ptr, length):
     data = (ctypes.c_char * length).from_address(ctypes.addressof(ptr.contents))
     return pickle.loads(data.raw)

@@ -159,6 +159,17 @@ def test_host_stage_auto_across_restart(mock):
     assert "resumed at version" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("world,args", [(2, []), (4, []), (3, ["rabit_device_allgather_resolve=0"])])
+def test_allgather_layout_resolved_on_device(world, args):
+    """device Allgather over the direct transport with no host round for the slice layout:
+    variable, wrapping, repeated and changed slices over several stage windows, byte-exact"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("allgather_resolved.py", world, args)
+    assert rc == 0, out[-5000:]
+    assert out.count("AGRESOLVED OK") == world, out[-3000:]
+
+
 def test_recovery_epoch_adopts_calibration():
     """after a kill, the next device epoch takes the survivors' calibration (one verified op per
     transport) instead of re-measuring it, on the restarted rank as on the survivors"""
