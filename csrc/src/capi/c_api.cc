@@ -94,6 +94,9 @@ rabit::engine::mpi::OpType ToOp(int o) {
 }  // namespace
 
 RABIT_DLL bool RabitInit(int argc, char *argv[]) {
+  // a process driven through the C API ends on a native error (Guard): a mock kill then ends it
+  // at once, like a crash, instead of unwinding the stack first
+  rabit::engine::SetMockKillsExit(g_error_mode == 0);
   return Guard([&]() { return rabit::Init(argc, argv); }, false);
 }
 
@@ -209,7 +212,10 @@ RABIT_DLL int RabitGetDevice() { return rabit::GetDevice(); }
 
 RABIT_DLL int RabitIsDevicePointer(const void *ptr) { return rabit::IsDevicePointer(ptr) ? 1 : 0; }
 
-RABIT_DLL void RabitSetErrorMode(int mode) { g_error_mode = mode; }
+RABIT_DLL void RabitSetErrorMode(int mode) {
+  g_error_mode = mode;
+  rabit::engine::SetMockKillsExit(mode == 0);
+}
 
 RABIT_DLL void RabitDevAllreducePrepared(void *dst, const void *src, size_t count,
                                          int enum_dtype, int enum_op, int prep_op,

@@ -30,6 +30,16 @@ using net::Status;
 typedef IEngine::ReduceFunction *ReduceFn;
 
 /*! \brief per-engine counters exported by RabitGetStats */
+/*!
+ * \brief mock kills end the process immediately (print, then _Exit as the C API's fatal-error
+ *        path does) instead of throwing.  Set by the C API for processes that exit on errors
+ *        anyway: the throw would only unwind the stack first, which costs ~0.3 s in a process
+ *        with torch's libraries loaded and delays the survivors' detection.  C++ programs and the
+ *        unit tests keep the reference's throw (`src/allreduce_mock.h:196-202`).
+ */
+void SetMockKillsExit(bool v);
+bool MockKillsExit();
+
 struct EngineStats {
   uint64_t n_allreduce{0}, n_broadcast{0}, n_allgather{0}, n_checkpoint{0};
   uint64_t n_device_ops{0}, n_recovered_ops{0}, n_recover_events{0}, n_consensus{0};

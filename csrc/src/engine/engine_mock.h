@@ -233,6 +233,13 @@ class EngineMock : public EngineRobust {
       fflush(stderr);
       for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
     }
+    if (MockKillsExit()) {
+      fprintf(stderr, "[xrabit] [%d]@@@Hit Mock Error:%s\nxrabit: fatal: [%d]@@@Hit Mock Error:%s\n",
+              rank_, what, rank_, what);
+      fflush(stderr);
+      fflush(stdout);
+      std::_Exit(254);
+    }
     utils::Error("[%d]@@@Hit Mock Error:%s", rank_, what);
   }
   int num_trial_{0};

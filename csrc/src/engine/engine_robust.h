@@ -293,7 +293,8 @@ class EngineRobust : public EngineBase {
   std::atomic<int> wd_rank_{-1};  // rank as seen by the watchdog thread (rank_ is not atomic)
   double hang_timeout_sec_{0};    // rabit_hang_timeout_sec (0: off)
   double attempt_start_{0};       // start of the current op attempt (recovery phase "detect")
-  double recover_stagger_ms_{10}; // rabit_recover_stagger_ms: reconnect delay per rank
+  double recover_stagger_ms_{2};  // rabit_recover_stagger_ms: reconnect delay per rank (the
+                                  // reference: 10; our tracker serves reconnects concurrently)
 };
 }  // namespace engine
 }  // namespace rabit

@@ -10,6 +10,7 @@
  * Unlike the reference, Allreduce_ keeps the dtype/op enums (AllreduceTyped) so device
  * buffers can use RCCL and the CDNA4 kernels.
  */
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -29,6 +30,11 @@
 
 namespace rabit {
 namespace engine {
+namespace {
+std::atomic<bool> g_mock_kills_exit{false};
+}  // namespace
+void SetMockKillsExit(bool v) { g_mock_kills_exit.store(v); }
+bool MockKillsExit() { return g_mock_kills_exit.load(); }
 
 void IEngine::AllreduceTyped(void *buf, size_t count, mpi::DataType dtype, mpi::OpType op,
                              ReduceFunction reducer, PreprocFunction prepare_fun,

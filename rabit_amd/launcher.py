@@ -106,7 +106,7 @@ class LocalJob:
             if attempt >= self.num_attempt:
                 self.returncodes[task] = rc
                 return
-            time.sleep(0.05)
+            time.sleep(0.01)  # (a restart is on the recovery critical path of the survivors)
 
     def run(self) -> int:
         self.tracker.start(self.n)

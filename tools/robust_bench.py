@@ -78,20 +78,32 @@ def main():
         lo, hi = float(model.min()), float(model.max())
     model_ok = abs(lo - expect) <= 1e-4 * expect and abs(hi - expect) <= 1e-4 * expect
     st = rabit.stats()
+    # recovery cost, split (stats()["recovery_phases_s"]); the restarted rank's process start-up
+    # (interpreter, imports, rabit.init) is reported apart: it is the launcher's and Python's
+    ph = st.get("recovery_phases_s", {})
+    startup = ph.get("process_start_to_init", 0.0) if attempt > 0 else 0.0
+    startup = float(rabit.allreduce(np.array([startup]), rabit.MAX)[0])
+    worst = float(rabit.allreduce(np.array([max(iter_t) if iter_t else 0.0]), rabit.MAX)[0])
     rec = {"rank": rank, "world": world, "attempt": attempt, "device": gpu,
            "bytes": nbytes, "start_version": version,
            "iter_ms": [round(t * 1e3, 2) for t in iter_t],
            "checkpoint_ms": [round(t * 1e3, 3) for t in ckpt_t],
            "recoveries": st["n_recover_events"], "recovered_ops": st["n_recovered_ops"],
            "device_replays": st.get("n_device_replays", 0),
-           "model_check": {"ok": model_ok, "expect": expect, "min": lo, "max": hi}}
+           "model_check": {"ok": model_ok, "expect": expect, "min": lo, "max": hi},
+           "recovery_phases_s": ph}
     if attempt > 0:
         rec["restart_to_loaded_s"] = round(t_loaded - T_START, 3)
     if rank == 0 and iter_t:
         steady = sorted(iter_t)[: max(1, len(iter_t) - 2)]
         rec["summary"] = {"steady_iter_ms_median": round(float(np.median(steady)) * 1e3, 2),
                           "slowest_iter_ms": round(max(iter_t) * 1e3, 2),
-                          "checkpoint_ms_median": round(float(np.median(ckpt_t)) * 1e3, 3)}
+                          "checkpoint_ms_median": round(float(np.median(ckpt_t)) * 1e3, 3),
+                          # the iteration that absorbed the failure (max over ranks), less the
+                          # restarted process's start-up to rabit.init()
+                          "failure_iter_ms_max_over_ranks": round(worst * 1e3, 2),
+                          "restarted_startup_to_init_ms": round(startup * 1e3, 2),
+                          "failure_iter_minus_startup_ms": round((worst - startup) * 1e3, 2)}
     print("ROBUST " + json.dumps(rec), flush=True)
     rabit.finalize()
     if not model_ok:
