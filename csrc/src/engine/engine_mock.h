@@ -234,7 +234,8 @@ class EngineMock : public EngineRobust {
       for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
     }
     if (MockKillsExit()) {
-      fprintf(stderr, "[xrabit] [%d]@@@Hit Mock Error:%s\nxrabit: fatal: [%d]@@@Hit Mock Error:%s\n",
+      fprintf(stderr,
+              "[xrabit] [%d]@@@Hit Mock Error:%s\nxrabit: fatal: [%d]@@@Hit Mock Error:%s\n",
               rank_, what, rank_, what);
       fflush(stderr);
       fflush(stdout);
