@@ -667,6 +667,19 @@ def main():
     phase("warmup")
     for _ in range(args.warmup):
         rabit.allreduce(x, rabit.SUM)
+    # the steady-state path checked as well: by now the input is read in place by the peers
+    # (zero-copy registry) where the first check staged it; a wrong result turns zero copy off
+    zero_copy_check = None
+    if args.check and world > 1:
+        phase("check after warmup")
+        zero_copy_check = check_allreduce(rabit, x, rank, ref)
+        if not zero_copy_check:
+            rabit.set_zero_copy(0)
+            if not check_allreduce(rabit, x, rank, ref):
+                raise SystemExit("allreduce result check after the warm-up failed")
+        x.copy_(torch.rand((n,), generator=g, dtype=torch.float32, device=dev).mul_(1e-3))
+        for _ in range(2):
+            rabit.allreduce(x, rabit.SUM)
     phase("timed")
     elapsed, elapsed_mean = time_steps(rabit, torch, x, args.steps, with_mean=True)
     st_head = rabit.stats()
@@ -705,10 +718,14 @@ def main():
         "baseline_note": "reference publishes no numbers (BASELINE.md)",
         "result_check": "bit-exact vs host fp64 reference" if checked else None,
         "check_fallback": check_fallback,
+        "steady_state_check": (None if zero_copy_check is None else
+                               ("bit-exact" if zero_copy_check
+                                else "failed: zero copy turned off, then bit-exact")),
         "consensus_elided": st.get("n_consensus_elided", 0),
         "device_epoch": st.get("device_epoch", 0),
         "transport": {"rccl": st.get("device_rccl", 0), "direct": st.get("device_direct", 0),
                       "zero_copy_chunks": st.get("zero_copy_chunks", 0),
+                      "zero_copy_registry": st.get("zero_copy_registry"),
                       "direct_min_bytes": st.get("device_direct_min", -1),
                       "direct_below_bytes": st.get("device_direct_below", 0),
                       "calibration_us": st.get("calib_us"),

@@ -135,6 +135,12 @@ RABIT_DLL int RabitDevGraphAllreduce(void *buf, size_t count, int enum_dtype, in
  *        slot and buf (the robust engine's dual store), host wait; 2: in place, stream-ordered.
  * \return 0; -1 the op failed (no recovery: a probe); -2 no device plane
  */
+/*!
+ * \brief xrabit extension: ordinary HBM inputs of at least min_bytes are IPC-registered and
+ *        read in place by the direct transport's peers (0: never).  Every rank must make the
+ *        same call between the same collectives.  \return 0, -1 without a device plane
+ */
+RABIT_DLL int RabitDevSetZeroCopy(size_t min_bytes);
 RABIT_DLL int RabitDevProbeAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
                                      int mode);
 /*!

@@ -327,6 +327,13 @@ RABIT_DLL int RabitDevSetFused(int fused) {
   return 0;
 }
 
+RABIT_DLL int RabitDevSetZeroCopy(size_t min_bytes) {
+  rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();
+  if (e == nullptr || e->device_plane() == nullptr) return -1;
+  e->device_plane()->SetZeroCopyMin(min_bytes);
+  return 0;
+}
+
 RABIT_DLL int RabitDevProbeAllreduce(void *buf, size_t count, int enum_dtype, int enum_op,
                                      int mode) {
   rabit::engine::EngineBase *e = rabit::engine::GetEngineBase();

@@ -830,7 +830,14 @@ Status DevicePlane::WaitUntil(const Poll &poll, const FailureProbe &probe) {
     hipError_t e = poll();
     if (e == hipSuccess) {
       if (peers_ != nullptr && peers_->failed()) {
-        utils::HandleLogInfo("[xrabit] direct transport: a peer barrier gave up\n");
+        const int why = peers_->fail_reason();
+        utils::HandleLogInfo("[xrabit] direct transport: a peer barrier gave up "
+                             "(%s; registry %s)\n",
+                             why == 1   ? "abort raised"
+                             : why == 2 ? "a zero-copy source was not mapped"
+                             : why == 3 ? "deadline"
+                                        : "unknown",
+                             RegistryJson().c_str());
         if (force_ == 1) {
           DropPeers();  // calibration probe: keep the RCCL communicator
         } else {

@@ -373,6 +373,11 @@ class DevicePlane {
   size_t sym_heap_used() const { return heap_used_; }
   uint64_t zero_copy_chunks() const { return peers_ ? peers_->zero_copy_chunks() : 0; }
   uint64_t reg_zero_copy_chunks() const { return peers_ ? peers_->reg_zero_copy_chunks() : 0; }
+  /*! \brief ordinary inputs of at least this size are registered for zero copy (0: never) */
+  void SetZeroCopyMin(size_t b) {
+    cfg_.zero_copy_min = b;
+    if (peers_ != nullptr) peers_->set_zero_copy_min(b);
+  }
   /*! \brief zero-copy registry counters as JSON ({} without a peer group) */
   std::string RegistryJson() const;
   /*! \brief every rank opened the group: drop the names of the shared registry pages */

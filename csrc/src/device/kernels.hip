@@ -115,7 +115,49 @@ struct SrcList {
   int prep;                  // PrepOp applied to sources prep_from.. as they are loaded (the
   int prep_from;             // lazy prepare fused into the reduce: no separate pass)
   double prep_alpha;
+  int coherent;  // 1: sources are read with system-scope loads (see LoadSys16)
 };
+
+/*!
+ * \brief system-scope 16-byte load (buffer_load_dwordx4 sc0 sc1): never served from a cache line
+ *        another agent may have left stale.  The direct transport's pull reduce reads its peers'
+ *        inputs in place (zero copy, peer_registry.h) from ordinary cacheable HBM of another
+ *        process or GPU, written there by that rank's kernels; this GPU's L2 may still hold the
+ *        same addresses from the previous op.  (Stage buffers and the symmetric heap are uncached
+ *        anyway, where the scope changes nothing.)  Offsets are 32-bit: callers keep the source
+ *        below 2 GiB (one chunk of the stage at most).
+ */
+__device__ __forceinline__ uint4 LoadSys16(const void *base, size_t vec_index) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+  const u32x4_t v =
+      __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(vec_index * 16), 0, 1 | 16);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+/*! \brief element i of a source with a system-scope load (tails of LoadSys16 reads) */
+template <typename T>
+__device__ __forceinline__ T LoadSysElem(const void *base, size_t i) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+  const int off = static_cast<int>(i * sizeof(T));
+  T x;
+  if constexpr (sizeof(T) == 1) {
+    const unsigned char v = __builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 1 | 16);
+    __builtin_memcpy(&x, &v, 1);
+  } else if constexpr (sizeof(T) == 2) {
+    const unsigned short v = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 1 | 16);
+    __builtin_memcpy(&x, &v, 2);
+  } else if constexpr (sizeof(T) == 4) {
+    const unsigned int v = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 1 | 16);
+    __builtin_memcpy(&x, &v, 4);
+  } else {
+    typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 1 | 16);
+    __builtin_memcpy(&x, &v, 8);
+  }
+  return x;
+}
 
 /*! \brief source k: from the device table when given (written by an earlier kernel, e.g. a
  *  peer barrier that resolved where each peer's input lives), else the launch argument */
@@ -131,7 +173,8 @@ __device__ __forceinline__ bool Guarded(const int *guard) {
 /*! \brief scalar form of ReduceVecs over nsrc sources (tails, unaligned buffers) */
 template <typename T>
 __device__ __forceinline__ T LoadSrc(const SrcList &srcs, int k, size_t i) {
-  const T x = static_cast<const T *>(Src(srcs, k))[i];
+  const T x = srcs.coherent ? LoadSysElem<T>(Src(srcs, k), i)
+                            : static_cast<const T *>(Src(srcs, k))[i];
   return srcs.prep != 0 && k >= srcs.prep_from
              ? PrepApply<T>(x, srcs.prep, static_cast<T>(srcs.prep_alpha))
              : x;
@@ -164,8 +207,13 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) {
       const uint4 *sk = reinterpret_cast<const uint4 *>(Src(srcs, k));
+      if (srcs.coherent) {  // uniform branch
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[k][u] = sk[base + u * kBlock];
+        for (int u = 0; u < U; ++u) x[k][u] = LoadSys16(sk, base + u * kBlock);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[k][u] = sk[base + u * kBlock];
+      }
     }
     if (srcs.prep != 0) {  // uniform branch: the fused lazy prepare, applied on load
 #pragma unroll
@@ -193,7 +241,8 @@ __global__ __launch_bounds__(kBlock) void ReduceMultiTileKernel(T *dst, SrcList 
       uint4 v[NSRC];
 #pragma unroll
       for (int k = 0; k < NSRC; ++k) {
-        v[k] = reinterpret_cast<const uint4 *>(Src(srcs, k))[i];
+        v[k] = srcs.coherent ? LoadSys16(Src(srcs, k), i)
+                             : reinterpret_cast<const uint4 *>(Src(srcs, k))[i];
         if (srcs.prep != 0 && k >= srcs.prep_from) {
           v[k] = PrepVec<T>(v[k], srcs.prep, static_cast<T>(srcs.prep_alpha));
         }
@@ -240,6 +289,8 @@ hipError_t ReduceMulti(void *dst, const void *const *srcs, int nsrc, size_t n, h
   sl.prep = prep;
   sl.prep_from = prep_from;
   sl.prep_alpha = prep_alpha;
+  // sources resolved on the device (a barrier's table) may be peers' inputs read in place
+  sl.coherent = table != nullptr && n * sizeof(T) < (size_t(1) << 31) ? 1 : 0;
   bool aligned = Aligned16(dst) && (dst2 == nullptr || Aligned16(dst2));
   for (int k = 0; k < kMaxReduceSources; ++k) {
     sl.p[k] = k < nsrc ? srcs[k] : nullptr;

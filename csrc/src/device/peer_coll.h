@@ -317,6 +317,10 @@ class PeerGroup {
   void SignalAbort();
   /*! \brief true when a barrier gave up (read after the stream drained) */
   bool failed() const;
+  /*! \brief why the group failed: 1 abort word, 2 unmapped zero-copy source, 3 deadline */
+  int fail_reason() const {
+    return host_words_ != nullptr ? __atomic_load_n(&host_words_[1], __ATOMIC_SEQ_CST) : 0;
+  }
   uint64_t barriers() const { return epoch_; }
   /*! \brief chunks whose input was read in place (symmetric heap or a registered allocation:
    *  no stage copy) */

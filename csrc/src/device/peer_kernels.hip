@@ -89,8 +89,10 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       if (*abort_word != 0 || wall_clock64() - t0 > deadline_ticks) {
-        __hip_atomic_store(dev_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the reason, for the host's log: 1 the host raised the abort word, 3 the deadline
+        const int why = *abort_word != 0 ? 1 : 3;
+        __hip_atomic_store(dev_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(4);
@@ -122,8 +124,8 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
         if (base == nullptr) {
           // cannot happen by the protocol; fail the op (the group is rebuilt) instead of
           // reading through a null mapping
-          __hip_atomic_store(dev_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(host_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dev_status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(host_status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           return;
         }
         src = base + (m & kMailboxOffsetMask);

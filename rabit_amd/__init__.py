@@ -17,6 +17,6 @@ from .core import (BITOR, DTYPE_ENUM, DTYPE_ENUM__, MAX, MIN, PREP_ABS, PREP_COP
                    checkpoint_tensors, load_checkpoint_tensors, symmetric_empty,
                    set_device_transport, set_phase_timing, allreduce_graphable, TRANSPORT_AUTO,
                    TRANSPORT_DIRECT, TRANSPORT_RCCL, link_probe, probe_allreduce,
-                   PROBE_BASE, PROBE_DUAL_STORE, PROBE_NO_WAIT)
+                   PROBE_BASE, PROBE_DUAL_STORE, PROBE_NO_WAIT, set_zero_copy)
 
 __version__ = "0.1.0"

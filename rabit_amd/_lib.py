@@ -121,6 +121,7 @@ def _declare(d: ctypes.CDLL) -> None:
         "RabitDevSetPhaseTiming": (c_int, [c_int]),
         "RabitDevLinkProbe": (c_int, [c_size_t, ctypes.POINTER(c_double), c_int]),
         "RabitDevProbeAllreduce": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int]),
+        "RabitDevSetZeroCopy": (c_int, [c_size_t]),
         "RabitGetLastError": (c_char_p, []),
         "RabitGetStats": (c_char_p, []),
         "RabitTraceDump": (c_int, [c_char_p]),

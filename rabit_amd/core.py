@@ -495,6 +495,14 @@ def link_probe(nbytes: int = 64 << 20) -> Optional[dict]:
     return {k: round(float(v), 2) for k, v in zip(LINK_PROBE_KEYS, out)}
 
 
+def set_zero_copy(min_bytes: int) -> bool:
+    """Ordinary HBM inputs of at least min_bytes are IPC-registered and read in place by the
+    direct transport's peers instead of being staged (default 1 MiB; 0 turns it off).  Every
+    rank must make the same call between the same collectives.  False without a device plane."""
+    _check_init()
+    return _LIB.RabitDevSetZeroCopy(int(min_bytes)) == 0
+
+
 PROBE_BASE, PROBE_DUAL_STORE, PROBE_NO_WAIT = 0, 1, 2
 
 
