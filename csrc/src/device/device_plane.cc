@@ -935,6 +935,21 @@ void *DevicePlane::Scratch(size_t bytes, int slot) {
   return scratch_[slot];
 }
 
+void *DevicePlane::PinnedScratch(size_t bytes) {
+  if (bytes > pinned_bytes_) {
+    if (pinned_ != nullptr) {
+      CheckHip(hipStreamSynchronize(stream_), "hipStreamSynchronize");  // (no copy in flight)
+      (void)hipHostFree(pinned_);
+      pinned_ = nullptr;
+      pinned_bytes_ = 0;
+    }
+    const size_t want = std::max<size_t>(bytes, 1u << 20);
+    CheckHip(hipHostMalloc(&pinned_, want, hipHostMallocDefault), "hipHostMalloc(staging)");
+    pinned_bytes_ = want;
+  }
+  return pinned_;
+}
+
 void DevicePlane::StageToHost(void *host, const void *dev, size_t bytes) {
   core::DeviceWaitScope on_gpu;
   CheckHip(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream_), "D2H");

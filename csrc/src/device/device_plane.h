@@ -460,6 +460,9 @@ class DevicePlane {
    */
   Status Exchange(const std::vector<ExchangeItem> &plan, size_t *bytes_in,
                   const FailureProbe &probe = FailureProbe());
+  /*! \brief reusable page-locked host buffer of at least bytes (grows, never shrinks): the
+   *  staging area of device ops whose reduction runs on the host (user reducers) */
+  void *PinnedScratch(size_t bytes);
   /*! \brief stage a host-reducer allreduce through pinned host memory */
   void StageToHost(void *host, const void *dev, size_t bytes);
   void StageToDevice(void *dev, const void *host, size_t bytes);

@@ -473,6 +473,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       ResolveArgs ra{};
       ra.my_mailbox = my_mailbox;
       ra.reg_table = registry_ok_ ? registry_.device_table() : nullptr;
+      ra.own_src = chunk_src;
       ra.parity = which;
       for (int p = 0; p < n_; ++p) {
         ra.stage_base[p] = peer_base_[p];
@@ -556,6 +557,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       ResolveArgs ra{};
       ra.my_mailbox = my_mailbox;
       ra.reg_table = registry_ok_ ? registry_.device_table() : nullptr;
+      ra.own_src = chunk_src;
       ra.parity = which;
       for (int p = 0; p < n_; ++p) {
         ra.stage_base[p] = peer_base_[p];

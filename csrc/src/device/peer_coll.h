@@ -97,7 +97,9 @@ struct ResolveArgs {
   size_t seg_off;                   // byte offset of this rank's segment in the chunk
   const void **table;               // out: n source pointers
   // registered allocations (peer_registry.h): [peer][slot] mapped bases, for kMailboxReg words
+  // of the peers; this rank's own registered input is own_src (the table maps peers only)
   const char *const *reg_table;
+  const char *own_src;
   // optional allgather slice layout: publish my_meta (begin, size) before signalling, and after
   // the wait copy every rank's pair into meta_table[2 p .. 2 p + 1] (device memory)
   unsigned long long my_meta[2];

@@ -121,6 +121,10 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
         const int slot = static_cast<int>((m >> kMailboxRegShift) & (kMaxRegs - 1));
         const char *base = resolve.reg_table != nullptr
                                ? resolve.reg_table[t * kMaxRegs + slot] : nullptr;
+        if (t == rank) {
+          // this rank's own input, in place (its mailbox offset is into its own allocation)
+          base = resolve.own_src - (m & kMailboxOffsetMask);
+        }
         if (base == nullptr) {
           // cannot happen by the protocol; fail the op (the group is rebuilt) instead of
           // reading through a null mapping

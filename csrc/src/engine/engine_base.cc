@@ -510,13 +510,14 @@ Status EngineBase::TryAllreduceDevice(const void *src, void *dst, const ReduceSp
     return dev_->Finish(MakeProbe());
   }
   if (!rccl_ok) {
-    // user-defined reducer (host function): stage through host memory
+    // user-defined reducer (host function): stage through the plane's reusable page-locked
+    // buffer (DMA at PCIe rate, no allocation per op), reduce on the host, copy back
     utils::Check(prep == device::kPrepCopy, "fused prepare needs a built-in reduction");
-    std::vector<uint64_t> tmp((bytes + 7) / 8);
-    dev_->StageToHost(tmp.data(), src, bytes);
-    Status s = TryAllreduceHost(tmp.data(), spec);
+    void *tmp = dev_->PinnedScratch(bytes);
+    dev_->StageToHost(tmp, src, bytes);
+    Status s = TryAllreduceHost(tmp, spec);
     if (s != Status::kSuccess) return s;
-    dev_->StageToDevice(dst, tmp.data(), bytes);
+    dev_->StageToDevice(dst, tmp, bytes);
     if (dst2 != nullptr) dev_->CopyDeviceAsync(dst2, dst, bytes);
     return dev_->Finish(MakeProbe());
   }

@@ -170,6 +170,27 @@ def test_allgather_layout_resolved_on_device(world, args):
     assert out.count("AGRESOLVED OK") == world, out[-3000:]
 
 
+# seeded chaos on the device path (4 ranks sharing the GPU, tests/scripts/device_ft.py: a Sum,
+# a Max and a 3-chunk broadcast per iteration, then an HBM checkpoint): 1-3 kill points per seed,
+# among them deaths of ranks that serve a replay or a checkpoint load (routing, device exchange)
+# (the seeds with a serving death among the first 15, plus two plain ones)
+DEVICE_CHAOS_SEEDS = [201, 202, 204, 205, 207, 209, 211, 212, 214, 208]
+
+
+@pytest.mark.parametrize("seed", DEVICE_CHAOS_SEEDS)
+def test_device_chaos(seed):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from chaos_points import draw
+    points = draw(seed, 4, 4, 3, wheres=(0, 3, 3, 1))
+    rc, out = _run("device_ft.py", 4, points, attempts=6, timeout=240)
+    if "Too many nodes went down" in out:
+        return  # every holder of some data died: the engine says so instead of hanging
+    assert rc == 0, "seed %d points %s\n%s" % (seed, points, out[-5000:])
+    assert out.count("DEVFT OK") == 4, "seed %d points %s\n%s" % (seed, points, out[-3000:])
+
+
 def test_recovery_epoch_adopts_calibration():
     """after a kill, the next device epoch takes the survivors' calibration (one verified op per
     transport) instead of re-measuring it, on the restarted rank as on the survivors"""
