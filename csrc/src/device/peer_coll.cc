@@ -327,6 +327,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // kernels hand tiles over one by one, with no last barrier: a peer dying inside one leaves some
   // tiles delivered and others not, so they never store the second destination themselves.
   const size_t last_off = count == 0 || !defer_second_ ? 0 : (count - 1) / chunk * chunk;
+  bool tail_signal = false;  // the second destination's tail copy carries the done signal
   size_t tail_end = last_off;  // [0, tail_end) reaches out2 through the guarded copy
   for (size_t off = 0; off < count; off += chunk) {
     const size_t c = std::min(chunk, count - off);
@@ -438,7 +439,10 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;
-      const bool signal = done_signal_ && count <= chunk;  // single-launch op
+      // single-launch op; with a deferred second destination the tail copy after it signals
+      // instead (the host must not see the op done before that copy is)
+      const bool signal = done_signal_ && count <= chunk && (out2 == nullptr || !defer_second_);
+      if (done_signal_ && count <= chunk && !signal) tail_signal = true;
       if (signal) {
         fa.done_count = done_count();
         fa.done_word = done_word();
@@ -604,7 +608,16 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
     CopyBatch b;
     NewBatch(&b);
     AddSeg(&b, out2, out, nullptr, tail_end * tn);
+    if (tail_signal) {
+      b.done_count = done_count();
+      b.done_word = done_word();
+      b.epoch = ++fused_epoch_;
+    }
     XRABIT_TRY_HIP(LaunchCopyBatch(b, stream_));
+    if (tail_signal) {
+      done_pending_ = true;
+      done_epoch_ = b.epoch;
+    }
   }
   timing_pending_ = timed && !did_fused;  // phases exist only in the classic form
   return hipSuccess;

@@ -80,6 +80,11 @@ struct CopyBatch {
   int n;
   const int *guard;  // optional device word: the launch does nothing when it is non-zero
   int remote;        // 1: every segment is remote (as CopySeg::remote)
+  // optional completion signal (as FusedAllreduceArgs::done_word): the last workgroup stores
+  // epoch into done_word once every workgroup is through, guarded launches included
+  unsigned int *done_count;
+  unsigned long long *done_word;
+  unsigned long long epoch;
 };
 
 /*!
@@ -452,6 +457,9 @@ class PeerGroup {
     b->n = 0;
     b->guard = dev_status();
     b->remote = 0;
+    b->done_count = nullptr;
+    b->done_word = nullptr;
+    b->epoch = 0;
   }
 
   int device_;

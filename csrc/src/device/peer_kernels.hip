@@ -187,7 +187,25 @@ __device__ __forceinline__ void PushTile(const CopySeg &g, size_t lo, size_t hi)
   }
 }
 
+__device__ __forceinline__ void CopyBatchBody(const CopyBatch &batch);
+
 __global__ __launch_bounds__(kBlock) void CopyBatchKernel(CopyBatch batch) {
+  CopyBatchBody(batch);
+  if (batch.done_word != nullptr && threadIdx.x == 0) {
+    // this workgroup's stores are complete before it counts in; the last one to count in
+    // re-arms the counter and tells the host (pinned word)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old =
+        __hip_atomic_fetch_add(batch.done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(batch.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(batch.done_word, batch.epoch, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+__device__ __forceinline__ void CopyBatchBody(const CopyBatch &batch) {
   if (batch.guard != nullptr &&
       __hip_atomic_load(batch.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
     return;
