@@ -161,12 +161,30 @@ hipError_t PeerRegistry::Refresh(uint64_t op, hipStream_t stream) {
       }
       mapped_gen_[q][k] = g;
       if (g == 0) continue;
+      // a mapping opened from the same handle bytes is an earlier allocation whose export was
+      // released (see the header): close it, or the runtime returns it for this handle
+      for (int k2 = 0; k2 < kMaxRegs; ++k2) {
+        if (k2 == k || mapped_[q][k2] == nullptr ||
+            std::memcmp(handle_[q][k2], &handle, sizeof(handle)) != 0) {
+          continue;
+        }
+        if (!drained) {
+          hipError_t e = hipStreamSynchronize(stream);
+          if (e != hipSuccess) return e;
+          drained = true;
+        }
+        (void)hipIpcCloseMemHandle(mapped_[q][k2]);
+        mapped_[q][k2] = nullptr;
+        host_table_[q * kMaxRegs + k2] = nullptr;
+        dirty = true;
+      }
       void *m = nullptr;
       if (hipIpcOpenMemHandle(&m, handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
         (void)hipGetLastError();
         continue;  // never acknowledged: the exporter keeps staging this allocation
       }
       mapped_[q][k] = static_cast<char *>(m);
+      std::memcpy(handle_[q][k], &handle, sizeof(handle));
       host_table_[q * kMaxRegs + k] = mapped_[q][k];
       dirty = true;
       ++imports_;
@@ -218,14 +236,20 @@ int PeerRegistry::FindOrExport(uintptr_t p, size_t bytes, uint64_t op) {
     bad_ids_.push_back(id);
     return -1;
   }
-  // a free slot, else the least recently used one (its peers remap at their next op)
-  int k = 0;
-  for (int j = 0; j < kMaxRegs; ++j) {
-    if (local_[j].gen == 0) {
-      k = j;
-      break;
+  // the slot of an earlier allocation at this address (freed and re-made: the peers drop the old
+  // mapping when they see the slot rewritten), else a free slot, else the least recently used
+  int k = -1;
+  for (int j = 0; j < kMaxRegs && k < 0; ++j) {
+    if (local_[j].gen != 0 && local_[j].base == base) k = j;
+  }
+  for (int j = 0; j < kMaxRegs && k < 0; ++j) {
+    if (local_[j].gen == 0) k = j;
+  }
+  if (k < 0) {
+    k = 0;
+    for (int j = 1; j < kMaxRegs; ++j) {
+      if (local_[j].last_use < local_[k].last_use) k = j;
     }
-    if (local_[j].last_use < local_[k].last_use) k = j;
   }
   RegistryPage::Slot &s = mine_->slot[k];
   const uint64_t g = s.gen.load(std::memory_order_relaxed);

@@ -19,6 +19,11 @@
  *    device table the barrier kernel resolves mailboxes with (an async copy on the group's
  *    stream), and acknowledge (generation, first op it is valid for) in ITS OWN page.  A mapping
  *    that is replaced is closed only after the stream drained, so no enqueued op still uses it.
+ *  - handles are compared byte for byte before a mapping is opened: an allocation freed by its
+ *    exporter releases its export, so a later allocation can come back with identical handle
+ *    bytes (the same descriptor number of the same process), and the runtime would hand out the
+ *    old mapping again -- stale memory.  The importer closes such a mapping first.  An exporter
+ *    whose allocation was re-made at the same address rewrites that allocation's slot.
  *  - an op is zero copy on the exporter when every peer acknowledged the slot's current
  *    generation for an op index at or below this one: every rank numbers its allreduces alike
  *    (collectives in one order), and the importer enqueued the table update before the kernels
@@ -124,6 +129,7 @@ class PeerRegistry {
   // importer state
   std::vector<uint64_t> seen_version_;
   char *mapped_[kMaxRegPeers][kMaxRegs]{};
+  char handle_[kMaxRegPeers][kMaxRegs][64]{};  // the IPC handle behind each mapping
   uint64_t mapped_gen_[kMaxRegPeers][kMaxRegs]{};
   const char **host_table_{nullptr};  // pinned mirror of the device table
   const char **dev_table_raw_{nullptr};
