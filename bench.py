@@ -735,6 +735,9 @@ def main():
                           ["pull-classic", "pull-fused", "push-classic", "push-fused",
                            "push-pipelined"],
                           st.get("calib_forms_us", []))),
+                      # every calibrated size x transport / direct form, and the routing bands
+                      # built from them (engine/routing.h); {} when the job did not calibrate
+                      "calibration_matrix": st.get("calib_matrix"),
                       "direct_pipeline": bool(st.get("direct_pipeline", 0)),
                       "pipelined_ops": st.get("pipelined_ops", 0),
                       "direct_fused": bool(st.get("direct_fused", 0)),

@@ -516,6 +516,10 @@ Status EngineBase::CalibrateDevice() {
         ok = 0;
         break;
       }
+      if (debug_) {
+        utils::HandleLogInfo("[%d] calibration %s %zu B: %.1f us\n", rank_, forms[f].name,
+                             pts[i] * 4, T(1 + f, i) * 1e6);
+      }
       // the latency point and the large point take different code paths: verify both
       if ((i == 0 || i == np - 1) && !verified(pts[i])) {
         form_ok[f] = 0;

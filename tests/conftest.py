@@ -33,6 +33,35 @@ def native_build():
     return os.path.join(ROOT, "build", "bin")
 
 
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """A GPU test that runs longer than a minute says so once a minute (on stderr): a long
+    multi-rank job keeps reporting which test it is in, and a hang names itself long before its
+    own timeout (the job's, or pytest's --timeout) ends it with the ranks' output."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import threading
+    import time
+
+    done = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not done.wait(60.0):
+            sys.stderr.write("\n[heartbeat] %s running for %.0f s\n"
+                             % (request.node.nodeid, time.time() - t0))
+            sys.stderr.flush()
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        done.set()
+        th.join(timeout=1.0)
+
+
 @pytest.fixture(scope="session")
 def gpu_available():
     import torch

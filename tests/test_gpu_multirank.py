@@ -206,7 +206,8 @@ def test_recovery_epoch_adopts_calibration():
 def test_calibration_flow(extra):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    rc, out = _run("calibrate_check.py", 3, extra)
+    # rabit_debug: each calibration point is logged, so a stalled run shows where it stood
+    rc, out = _run("calibrate_check.py", 3, extra + ["rabit_debug=1"], timeout=170)
     assert rc == 0, out[-5000:]
     assert out.count("CALIB OK") == 3, out[-3000:]
 

@@ -1,9 +1,21 @@
-# zero-copy registry diagnosis (2 ranks sharing the GPU), then the new GPU tests
+# The next GPU-box session; argv[1] picks it.
+#   s8: smoke, the N=1 bench, the driver-shaped N = 2 / 4 / 8 launches (ranks share the GPU)
+#   s9: calibrated N=4 bench (size sweep), zero-copy kernel trace, device allgather with and
+#       without the on-device layout, BASELINE config 5 at 8 ranks with the rank-3 kill
 set -u
-mkdir -p gpurun_out/r4_s6
-echo "== zc debug $(date +%T)"
-timeout -k 10 100 python -m rabit_amd.launcher -n 2 -- python -u tests/scripts/zero_copy_check.py rabit_debug=1 rabit_device_peer_timeout_sec=10 > gpurun_out/r4_s6/zc.log 2>&1
-rc=$?
-echo "zc rc=$rc"; grep -m5 "gave up" gpurun_out/r4_s6/zc.log; tail -5 gpurun_out/r4_s6/zc.log
-[ $rc -ne 0 ] && exit $rc
-OUT_NAME=r4_s6 GPU_K="zero_copy or allgather_layout or calibration or host_stage_auto or rccl_lifecycle or symmetric" STEPS="gtest" bash tools/gpu_run.sh
+case ${1:-s8} in
+  s7b)
+    # the GPU tests after the one that stalled in r4_s7, then s8
+    OUT_NAME=r4_s7b GPU_K="calibration_flow or symmetric_zero_copy or registered_zero_copy or gradient_buckets or bench_torchrun_shared_gpu or direct_half_precision or device_local_checkpoint_recovery or device_hang_detected or forced_rccl_on_shared or rccl_init_failure_falls_back or small_op_stress or rccl_lifecycle or test_gpu_recovery or test_recovery" \
+      STEPS="gtest" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s8 STEPS="smoke bench1 shared" bash tools/gpu_run.sh ;;
+  s8) OUT_NAME=r4_s8 STEPS="smoke bench1 shared" bash tools/gpu_run.sh ;;
+  s9)
+    OUT_NAME=r4_s9 GPU_K="calibration_flow" STEPS="gtest" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s9 SHARED_NS=4 XRABIT_PARAMS=rabit_device_calibrate_test=1 STEPS="shared" \
+      bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s9 STEPS="zctrace" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s9 CMD="python -m rabit_amd.launcher -n 4 -- python -u tests/scripts/allgather_resolved.py && python -m rabit_amd.launcher -n 4 -- python -u tests/scripts/allgather_resolved.py rabit_device_allgather_resolve=0" \
+      STEPS="cmd" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s9 STEPS="robust" bash tools/gpu_run.sh ;;
+esac

@@ -15,7 +15,9 @@
 #   shared    the driver's N = $SHARED_NS launches (torchrun, every rank on this box's one GPU)
 #   prof      rocprofv3 --kernel-trace --stats of the N=1 bench
 #   kbench    kernel bench against the measured HBM peak
-#   robust    tools/robust_bench.py config 5 (8 shared ranks, rank-3 kill) with phase breakdown
+#   robust    tools/robust_bench.py = BASELINE config 5 on $ROBUST_N (8) shared ranks: clean, then
+#             rank 3 killed at version 4 (restarted by the launcher), recovery phase breakdown
+#   zctrace   tools/zero_copy_trace.sh: kernel order with / without the zero-copy registry
 #   cmd       an arbitrary command: CMD="..." (limit CMD_LIMIT seconds, default 300)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -49,7 +51,13 @@ for s in ${STEPS:-tests smoke bench1}; do
     prof)   step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv \
               -d "$OUT/prof" -o bench -- python3 bench.py --steps 10 --warmup 3 ;;
     kbench) step kbench 300 python tools/kernel_bench.py ;;
-    robust) step robust 600 python -u tools/robust_bench.py ${ROBUST_ARGS:-} ;;
+    robust)
+      step robust_clean 260 env XR_ITERS=12 python -m rabit_amd.launcher -n ${ROBUST_N:-8} \
+        --num-attempt 1 --timeout 240 -- python -u tools/robust_bench.py ${ROBUST_ARGS:-}
+      step robust_kill 260 env XR_ITERS=12 python -m rabit_amd.launcher -n ${ROBUST_N:-8} \
+        --num-attempt 2 --timeout 240 -- python -u tools/robust_bench.py mock=3,4,0,0 \
+        ${ROBUST_ARGS:-} ;;
+    zctrace) step zctrace 300 bash tools/zero_copy_trace.sh ;;
     cmd)    step cmd 600 bash -c "${CMD:?set CMD}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
