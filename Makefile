@@ -27,7 +27,7 @@ HIPFLAGS  := $(OPT) -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics 
 # -z defs: a symbol declared but never defined fails the link, not the first dlopen
 LDLIBS    := -Wl,-z,defs -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrccl -lrocprofiler-sdk-roctx -pthread -Wl,-rpath,$(ROCM)/lib $(SAN)
 
-CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc csrc/src/net/link_reset.cc \
+CORE_SRCS := csrc/src/core/log.cc csrc/src/core/trace.cc csrc/src/core/exit.cc csrc/src/net/socket.cc csrc/src/net/tracker_client.cc csrc/src/net/link_reset.cc \
              csrc/src/coll/host_coll.cc csrc/src/coll/shm_coll.cc csrc/src/device/device_plane.cc csrc/src/device/device_checkpoint.cc csrc/src/device/dma_copier.cc csrc/src/device/peer_coll.cc csrc/src/device/peer_registry.cc csrc/src/device/host_stager.cc \
              csrc/src/engine/engine_base.cc csrc/src/engine/device_setup.cc csrc/src/engine/engine_robust.cc \
              csrc/src/engine/recovery.cc csrc/src/engine/local_replicas.cc csrc/src/engine/local_recovery.cc \

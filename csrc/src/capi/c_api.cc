@@ -20,6 +20,7 @@
 #include <string>
 
 #include "coll/host_coll.h"
+#include "core/exit.h"
 #include "core/trace.h"
 #include "device/kernels.h"
 #include "engine/engine_base.h"
@@ -45,9 +46,7 @@ auto Guard(F &&f, decltype(f()) fallback) -> decltype(f()) {
     g_last_error = e.what();
     if (g_error_mode == 0) {
       fprintf(stderr, "xrabit: fatal: %s\n", e.what());
-      fflush(stderr);
-      fflush(stdout);
-      std::_Exit(254);
+      rabit::utils::ExitProcess(254);
     }
     return fallback;
   }

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <thread>
 
+#include "core/exit.h"
 #include "core/trace.h"
 #include "core/wait_state.h"
 #include "device/kernels.h"
@@ -636,7 +637,7 @@ void DevicePlane::WedgedExit(const char *why) {
   // give them that time before the process and its queues go away (no blocking HIP call here:
   // a really wedged stream would never return from it)
   std::this_thread::sleep_for(std::chrono::milliseconds(200));
-  std::_Exit(kDeviceHangExitCode);
+  utils::ExitProcess(kDeviceHangExitCode);
 }
 
 bool DevicePlane::Preflight(const std::vector<PeerRecord> &all, int rank, std::string *why) {

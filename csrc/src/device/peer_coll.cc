@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "core/exit.h"
 #include "device/ar_plan.h"
 #include "device/bcast_plan.h"
 #include "device/device_plane.h"
@@ -735,7 +736,7 @@ void PeerGroup::DieMidOp() {
   fprintf(stderr, "[%d]@@@Hit Mock Die Mid Op: exiting inside a multi-chunk device allreduce\n",
           rank_);
   fflush(stderr);
-  std::_Exit(kMockDieMidExitCode);
+  utils::ExitProcess(kMockDieMidExitCode);
 }
 
 hipError_t PeerGroup::AllreducePipelined(const char *in, char *out, char *out2, size_t count,

@@ -34,6 +34,7 @@
 #include <thread>
 #include <tuple>
 
+#include "core/exit.h"
 #include "core/wait_state.h"
 #include "engine/engine_robust.h"
 #include "rabit/internal/timer.h"
@@ -177,7 +178,7 @@ class EngineMock : public EngineRobust {
             names[static_cast<int>(where)], version_number_, seq_counter_);
     fflush(stderr);
     // as a crash: no unwinding through the recovery code, no Finalize
-    std::_Exit(kMockDieServingExitCode);
+    utils::ExitProcess(kMockDieServingExitCode);
   }
   static constexpr int kMockDieServingExitCode = 249;
 
@@ -237,9 +238,7 @@ class EngineMock : public EngineRobust {
       fprintf(stderr,
               "[xrabit] [%d]@@@Hit Mock Error:%s\nxrabit: fatal: [%d]@@@Hit Mock Error:%s\n",
               rank_, what, rank_, what);
-      fflush(stderr);
-      fflush(stdout);
-      std::_Exit(254);
+      utils::ExitProcess(254);
     }
     utils::Error("[%d]@@@Hit Mock Error:%s", rank_, what);
   }

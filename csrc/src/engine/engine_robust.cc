@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "core/exit.h"
 #include "core/trace.h"
 #include "core/wait_state.h"
 #include "device/kernels.h"
@@ -795,7 +796,7 @@ void EngineRobust::WatchdogLoop() {
               "(rabit_hang_timeout_sec=%g): exiting for a restart\n",
               wd_rank_.load(), working, hang_timeout_sec_);
       fflush(stderr);
-      std::_Exit(kHangExitCode);
+      utils::ExitProcess(kHangExitCode);
     }
     // a wait on this rank's own GPU that outlasts every deadline (a HIP call that blocks on a
     // wedged stream): nothing in this process can unblock it, so leave for a restart
@@ -822,7 +823,7 @@ void EngineRobust::WatchdogLoop() {
         fprintf(stderr, "[%d] xrabit: recovery did not finish within %d s, exiting\n", rank,
                 timeout_sec_);
         fflush(stderr);
-        std::_Exit(253);
+        utils::ExitProcess(253);
       }
     }
   }

@@ -67,6 +67,50 @@ def test_launcher_restarts_failing_worker(tmp_path):
     assert flag.exists() and job.attempts == [1, 2]
 
 
+def test_launcher_restarts_on_reported_exit(tmp_path):
+    """a worker that reports its exit code on the launcher's exit pipe is replaced at once, while
+    it is still tearing down (here: sleeping 3 s before it really exits)"""
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "t = int(os.environ['DMLC_TASK_ID']); a = int(os.environ['DMLC_NUM_ATTEMPT'])\n"
+        "if t == 1 and a == 0:\n"
+        "    fd = int(os.environ['XRABIT_EXIT_FD'].split(':')[0])\n"
+        "    open(%r, 'w').write(repr(time.time()))\n"
+        "    os.write(fd, b'7\\n'); time.sleep(3); sys.exit(7)\n"
+        "if t == 1:\n"
+        "    open(%r, 'w').write(repr(time.time()))\n"
+        % (str(tmp_path / "died"), str(tmp_path / "again")))
+    job = LocalJob([sys.executable, str(script)], 2, 3, timeout=60, print_fn=lambda m: None)
+    job.tracker.start = lambda n: None  # no rabit.init in this worker: no tracker needed
+    job.tracker.join = lambda t: None
+    assert job.run() == 0
+    died = float((tmp_path / "died").read_text())
+    again = float((tmp_path / "again").read_text())
+    assert again - died < 2.0, again - died
+    assert job.attempts == [1, 2] and job.reported_exits == [[], [7]]
+
+
+def test_mock_kill_reports_exit_code(tmp_path):
+    """the native mock kill shuts its sockets and reports its code on the exit pipe
+    (csrc/src/core/exit.h) before it _Exits; the job still ends with the exact result"""
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import numpy as np\n"
+        "import rabit_amd as rabit\n"
+        "rabit.init(sys.argv[1:], lib='mock')\n"
+        "v, _ = rabit.load_checkpoint()\n"
+        "x = rabit.allreduce(np.ones(4) * (rabit.get_rank() + 1), rabit.SUM)\n"
+        "assert x[0] == 3, x\n"
+        "rabit.finalize()\n" % ROOT)
+    job = LocalJob([sys.executable, str(script), "mock=1,0,0,0"], 2, 3, timeout=60,
+                   print_fn=lambda m: None)
+    assert job.run() == 0
+    assert job.reported_exits == [[], [254]] and job.attempts == [1, 2]
+
+
 def test_launcher_cli_basic_example(native_build):
     out = subprocess.run([sys.executable, "-m", "rabit_amd.launcher", "-n", "3", "--",
                           os.path.join(native_build, "basic")], capture_output=True, text=True,

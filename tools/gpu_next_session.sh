@@ -11,11 +11,14 @@ case ${1:-s8} in
     OUT_NAME=r4_s8 STEPS="smoke bench1 shared" bash tools/gpu_run.sh ;;
   s8) OUT_NAME=r4_s8 STEPS="smoke bench1 shared" bash tools/gpu_run.sh ;;
   s9)
-    OUT_NAME=r4_s9 GPU_K="calibration_flow" STEPS="gtest" bash tools/gpu_run.sh || exit $?
-    OUT_NAME=r4_s9 SHARED_NS=4 XRABIT_PARAMS=rabit_device_calibrate_test=1 STEPS="shared" \
-      bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s9 STEPS="zctrace" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s9 CMD="python -m rabit_amd.launcher -n 4 -- python -u tests/scripts/allgather_resolved.py && python -m rabit_amd.launcher -n 4 -- python -u tests/scripts/allgather_resolved.py rabit_device_allgather_resolve=0" \
       STEPS="cmd" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s9 STEPS="robust" bash tools/gpu_run.sh ;;
+  s10)
+    # recovery with the exit pipe (sockets shut and the launcher told before _Exit), then the
+    # GPU fault-tolerance tests that restart workers through the launcher
+    OUT_NAME=r4_s10 STEPS="robust" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s10 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts" \
+      STEPS="gtest" bash tools/gpu_run.sh ;;
 esac

@@ -25,6 +25,16 @@ T_START = time.time()
 import rabit_amd as rabit  # noqa: E402
 
 
+def process_created():
+    """epoch time this process was created, to the kernel's clock tick (psutil's create_time
+    rounds the boot time to whole seconds)"""
+    with open("/proc/self/stat") as f:
+        start_ticks = int(f.read().rsplit(")", 1)[1].split()[19])  # field 22: starttime
+    with open("/proc/uptime") as f:
+        up = float(f.read().split()[0])
+    return time.time() - (up - start_ticks / os.sysconf("SC_CLK_TCK"))
+
+
 def main():
     args = [a for a in sys.argv[1:] if "=" in a]
     iters = int(os.environ.get("XR_ITERS", "10"))
@@ -46,9 +56,10 @@ def main():
         version, state = rabit.load_checkpoint()
         model = state if version else np.zeros(n, dtype=np.float32)
     t_loaded = time.time()
-    iter_t, ckpt_t = [], []
+    iter_t, ckpt_t, iter_t0 = [], [], []
     for it in range(version, iters):
         t0 = time.time()
+        iter_t0.append(t0)
         if gpu:
             grad = model * 1e-3 + rank
             rabit.allreduce(grad, rabit.SUM)
@@ -84,6 +95,14 @@ def main():
     startup = ph.get("process_start_to_init", 0.0) if attempt > 0 else 0.0
     startup = float(rabit.allreduce(np.array([startup]), rabit.MAX)[0])
     worst = float(rabit.allreduce(np.array([max(iter_t) if iter_t else 0.0]), rabit.MAX)[0])
+    # the restart timeline (epoch seconds): when the failure iteration began on the survivors,
+    # when the replacement process was created, when it had loaded its checkpoint, and its own
+    # first iteration
+    created = process_created() if attempt > 0 else 0.0
+    fail_t0 = iter_t0[int(np.argmax(iter_t))] if iter_t and attempt == 0 else 0.0
+    tl = rabit.allreduce(np.array([created, t_loaded if attempt > 0 else 0.0,
+                                   iter_t[0] if iter_t and attempt > 0 else 0.0, fail_t0]),
+                         rabit.MAX)
     rec = {"rank": rank, "world": world, "attempt": attempt, "device": gpu,
            "bytes": nbytes, "start_version": version,
            "iter_ms": [round(t * 1e3, 2) for t in iter_t],
@@ -104,6 +123,14 @@ def main():
                           "failure_iter_ms_max_over_ranks": round(worst * 1e3, 2),
                           "restarted_startup_to_init_ms": round(startup * 1e3, 2),
                           "failure_iter_minus_startup_ms": round((worst - startup) * 1e3, 2)}
+        if tl[0] > 0:
+            # failure iteration = respawn + start-up to init + init to loaded + the
+            # replacement's first iteration (+ the survivors' own wait to finish it)
+            rec["summary"]["restart_timeline_ms"] = {
+                "iteration_start_to_respawn": round((tl[0] - tl[3]) * 1e3, 1),
+                "respawn_to_init": round(startup * 1e3, 1),
+                "init_to_checkpoint_loaded": round((tl[1] - tl[0] - startup) * 1e3, 1),
+                "restarted_first_iteration": round(tl[2] * 1e3, 1)}
     print("ROBUST " + json.dumps(rec), flush=True)
     rabit.finalize()
     if not model_ok:

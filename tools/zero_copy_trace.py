@@ -9,8 +9,9 @@ the base engine (no result-log copies, so every CopyTileKernel is a stage copy) 
 two host barriers (rabit.allreduce of a 1-int host array, no device kernel) and its wall time is
 recorded.
 
-Analysis (`--analyze <kernel_trace.csv> <worker log>`): the kernels of each op's window, in start
-order: how many CopyTileKernel ran before its first PeerBarrierKernel.
+Analysis (`--analyze <kernel_trace.csv> <worker log> [out.json]`): the rabit kernels of each op in
+start order, the op's GPU span, and how many CopyTileKernel ran before its first
+PeerBarrierKernel.
 """
 import csv
 import json
@@ -19,6 +20,9 @@ import sys
 import time
 
 OPS = 10
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
 
 
 def worker():
@@ -56,7 +60,15 @@ def worker():
     ctx.finalize()
 
 
+def short_name(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0].split("<")[0].split("::")[-1]
+
+
 def analyze(trace_csv, log):
+    """each op of the worker is one run of consecutive rabit kernels between torch's own (the
+    input fill before it, the check after it) that contains a barrier; the last 2 x OPS such runs
+    are the timed ops, in order (zero copy on, then off)"""
     marks = None
     for line in open(log, encoding="utf-8", errors="replace"):
         if line.startswith("ZCTRACE "):
@@ -68,31 +80,37 @@ def analyze(trace_csv, log):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    # the trace's clock and time.time_ns differ by an offset: align on the first op's first
-    # barrier kernel (the op window's first kernel after the host barrier)
+    runs, cur = [], []
+    for s, e, name in rows:
+        if "rabit::device" in name:
+            cur.append((s, e, short_name(name)))
+        elif cur:
+            runs.append(cur)
+            cur = []
+    if cur:
+        runs.append(cur)
+    runs = [r for r in runs if any(k[2] == "PeerBarrierKernel" for k in r)]
+    windows = marks["marks"]
+    if len(runs) < len(windows):
+        raise SystemExit("%d ops in the trace, %d timed" % (len(runs), len(windows)))
+    runs = runs[-len(windows):]
     out = {"rank": marks["rank"], "world": marks["world"], "registry": marks["registry"],
            "ops": []}
-    windows = marks["marks"]
-    t_first = windows[0]["t0_ns"]
-    k0 = next(s for s, _, name in rows if "PeerBarrierKernel" in name or "CopyTileKernel" in name)
-    off = k0 - t_first
-    for w in windows:
-        lo, hi = w["t0_ns"] + off - 20000, w["t1_ns"] + off + 20000
-        names = [name for s, _, name in rows if lo <= s <= hi]
-        first_bar = next((i for i, nm in enumerate(names) if "PeerBarrierKernel" in nm), len(names))
-        short = [nm.split("(")[0].split("<")[0].replace("void ", "").replace("rabit::device::", "")
-                 for nm in names]
-        out["ops"].append({"zero_copy": w["zero_copy"], "op": w["op"], "us": round(w["us"], 1),
-                           "stage_copies_before_first_barrier": sum(
-                               1 for nm in names[:first_bar] if "CopyTileKernel" in nm),
-                           "stage_copies": sum(1 for nm in names if "CopyTileKernel" in nm),
-                           "kernels": short})
+    for w, run in zip(windows, runs):
+        names = [k[2] for k in run]
+        first_bar = names.index("PeerBarrierKernel")
+        out["ops"].append({
+            "zero_copy": w["zero_copy"], "op": w["op"], "wall_us": round(w["us"], 1),
+            "gpu_span_us": round((run[-1][1] - run[0][0]) / 1e3, 1),
+            "stage_copies_before_first_barrier": names[:first_bar].count("CopyTileKernel"),
+            "kernels": names})
     for zc in (1, 0):
         ops = [o for o in out["ops"] if o["zero_copy"] == zc and o["op"] >= 2]
-        ts = sorted(o["us"] for o in ops)
+        spans = sorted(o["gpu_span_us"] for o in ops)
         out["zero_copy_on" if zc else "zero_copy_off"] = {
-            "median_us_ops_2_on": ts[len(ts) // 2] if ts else None,
-            "stage_copies_per_op_ops_2_on": [o["stage_copies"] for o in ops]}
+            "median_gpu_span_us_ops_2_on": spans[len(spans) // 2] if spans else None,
+            "stage_copies_before_first_barrier_ops_2_on":
+                [o["stage_copies_before_first_barrier"] for o in ops]}
     return out
 
 
@@ -105,9 +123,10 @@ if __name__ == "__main__":
             with open(dst, "w") as f:
                 f.write(text + "\n")
         print(json.dumps({k: v for k, v in res.items() if k != "ops"}))
-        first = [o for o in res["ops"] if o["op"] in (0, 2)]
-        for o in first:
-            print(o["zero_copy"], o["op"], o["us"], " ".join(o["kernels"]))
+        for o in res["ops"]:
+            if o["op"] in (0, 2):
+                print("zero_copy=%d op %d: %.1f us: %s" % (o["zero_copy"], o["op"],
+                                                          o["gpu_span_us"], " ".join(o["kernels"])))
     else:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         worker()

@@ -15,7 +15,7 @@ for r in 0 1; do
 done
 rc=0
 for p in "${pids[@]}"; do wait "$p" || rc=$?; done
-[ $rc -ne 0 ] && { tail -20 "$OUT"/rank*.log; exit $rc; }
+[ $rc -ne 0 ] && { tail -n 20 "$OUT"/rank*.log; exit $rc; }
 for r in 0 1; do
   csvf=$(find "$OUT/r$r" -name '*kernel_trace.csv' | head -1)
   python3 tools/zero_copy_trace.py --analyze "$csvf" "$OUT/rank$r.log" "$OUT/rank${r}_ops.json" \
