@@ -405,6 +405,8 @@ class DevicePlane {
     return true;
   }
   int fused_grid() const { return peers_ ? peers_->fused_grid() : 0; }
+  /*! \brief ranks of the direct group share a GPU (a rehearsal or test setup) */
+  bool peers_share_gpu() const { return peers_ && peers_->gpu_share() > 1; }
   /*! \brief fill PeerRecord host/pci fields only (ranks without a peer group) */
   void DescribeDevice(PeerRecord *rec) const;
 

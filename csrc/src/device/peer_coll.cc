@@ -225,6 +225,7 @@ bool PeerGroup::Open(const std::vector<PeerRecord> &all, int rank, std::string *
   for (int a = 0; a < n; ++a) {
     if (all[a].fused_cap > 0) cap = std::min(cap, static_cast<int>(all[a].fused_cap));
   }
+  gpu_share_ = share;
   fused_grid_ = fused_grid_req_ > 0 ? fused_grid_req_ : std::max(16, cap / share);
   opened_ = true;
   return true;

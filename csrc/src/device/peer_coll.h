@@ -389,6 +389,8 @@ class PeerGroup {
   /*! \brief chunks below this many bytes keep the classic form */
   void set_fused_min_bytes(size_t b) { fused_min_bytes_ = b; }
   int fused_grid() const { return fused_grid_; }
+  /*! \brief the most ranks of this group on one GPU (1: every rank has its own) */
+  int gpu_share() const { return gpu_share_; }
   uint64_t fused_chunks() const { return fused_chunks_; }
   /*!
    * \brief the op just enqueued ends with a kernel that signals its completion in pinned host
@@ -502,7 +504,7 @@ class PeerGroup {
   bool fused_{true};
   size_t fused_oneshot_max_{64u << 10};
   uint64_t fused_oneshots_{0};
-  int fused_grid_req_{0}, fused_grid_{256};
+  int fused_grid_req_{0}, fused_grid_{256}, gpu_share_{1};
   size_t fused_min_bytes_{0};
   int tiles_cap_{0};                // flag slots per array of a fused flag block
   size_t fused_block_bytes_{0};     // bytes of one fused flag block (2 per allocation)

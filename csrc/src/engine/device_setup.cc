@@ -560,6 +560,14 @@ Status EngineBase::CalibrateDevice() {
       for (int i = 0; i < np; ++i) T(1 + f, i) = -1.0;
     }
   }
+  // A fused form hands tiles between the ranks' workgroups, so it needs every rank's grid
+  // resident at once.  Ranks on separate GPUs have that; ranks sharing one GPU (rehearsals,
+  // tests) do not -- the hardware time-slices separate processes' queues and other kernels hold
+  // slots -- and a fused op there can wait out the peer deadline.  Its times are reported, but
+  // nothing is routed to it.
+  const bool shared_gpu = dev_->peers_share_gpu();
+  std::vector<int> routable(nf, 1);
+  for (int f = 0; f < nf; ++f) routable[f] = form_ok[f] && !(shared_gpu && forms[f].fused);
   std::ostringstream js;
   js << "{\"bytes\":[";
   for (int i = 0; i < np; ++i) js << (i ? "," : "") << pts[i] * 4;
@@ -573,7 +581,11 @@ Status EngineBase::CalibrateDevice() {
     }
     js << "]";
   }
-  js << "}";
+  js << "},\"unrouted_forms\":[";
+  for (int f = 0, k = 0; f < nf; ++f) {
+    if (form_ok[f] && !routable[f]) js << (k++ ? "," : "") << "\"" << forms[f].name << "\"";
+  }
+  js << "]";
   size_t threshold = static_cast<size_t>(-1);
   int best_big = -1;  // direct form fastest at the large point
   if (!ok) {
@@ -585,7 +597,7 @@ Status EngineBase::CalibrateDevice() {
     std::vector<std::vector<double>> all(nc, std::vector<double>(np));
     std::vector<std::vector<double>> direct(nf, std::vector<double>(np));
     for (int c = 0; c < nc; ++c) {
-      for (int i = 0; i < np; ++i) all[c][i] = T(c, i);
+      for (int i = 0; i < np; ++i) all[c][i] = c == 0 || routable[c - 1] ? T(c, i) : -1.0;
     }
     for (int f = 0; f < nf; ++f) direct[f] = all[1 + f];
     const std::vector<RouteBand> tb = ChooseRoutes(xs, all);
@@ -601,7 +613,7 @@ Status EngineBase::CalibrateDevice() {
           device::DevicePlane::RouteChoice{static_cast<size_t>(b.lo), 1, f.push, f.pipe, f.fused});
     }
     for (int f = 0; f < nf; ++f) {
-      if (form_ok[f] && (best_big < 0 || T(1 + f, np - 1) < T(1 + best_big, np - 1))) best_big = f;
+      if (routable[f] && (best_big < 0 || T(1 + f, np - 1) < T(1 + best_big, np - 1))) best_big = f;
     }
     if (best_big < 0) best_big = 0;
     dev_->SetRoutes(tbands, fbands);  // (clears the forced form)
