@@ -690,6 +690,7 @@ void EngineRobust::CheckPointImpl(const Serializable *global_model,
                            cur_cache_seq_, "CheckPoint"),
                "check point must return true");
   version_number_ += 1;
+  ckpt_header_only_ = false;
   if (lazy) {
     global_lazycheck_ = global_model;
   } else {

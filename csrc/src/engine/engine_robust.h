@@ -281,6 +281,9 @@ class EngineRobust : public EngineBase {
   ResultLog resbuf_, cachebuf_, lookupbuf_;
   std::string global_checkpoint_;
   const Serializable *global_lazycheck_{nullptr};
+  // global_checkpoint_ holds only the version and header of a device-route load (the payload
+  // went into the caller's tensors): this rank cannot serve the checkpoint over TCP
+  bool ckpt_header_only_{false};
   LocalReplicas local_;
   // watchdog
   TimeoutHandler timeout_handler_{nullptr};

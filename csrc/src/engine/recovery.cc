@@ -463,6 +463,12 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
     s = TryLoadDeviceCheckPoint(role);
     if (s != Status::kAborted) return s;  // kAborted here: not applicable, use the TCP route
   }
+  // A rank that loaded this version over the device route keeps only its header: the payload
+  // went into the caller's tensors, which the caller has changed since.  On the TCP route it
+  // relays; offering the header as the checkpoint would hand requesters a truncated model (or,
+  // next to a real holder, fail the routing on two sizes).
+  const RecoverType tcp_role =
+      role == kHaveData && global_lazycheck_ == nullptr && ckpt_header_only_ ? kPassData : role;
   if (role == kHaveData && global_lazycheck_ != nullptr) {
     // materialise a lazy checkpoint now that a peer needs the bytes
     global_checkpoint_.clear();
@@ -474,11 +480,14 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
   size_t size = global_checkpoint_.length();
   int recv_link;
   std::vector<bool> req_in;
-  s = TryDecideRouting(role, &size, &recv_link, &req_in);
+  s = TryDecideRouting(tcp_role, &size, &recv_link, &req_in);
   if (s != Status::kSuccess) return s;
-  if (role == kRequestData) global_checkpoint_.resize(size);
+  if (role == kRequestData) {
+    global_checkpoint_.resize(size);
+    ckpt_header_only_ = false;
+  }
   if (size == 0) return Status::kSuccess;
-  return TryRecoverData(role, BeginPtr(global_checkpoint_), size, recv_link, req_in);
+  return TryRecoverData(tcp_role, BeginPtr(global_checkpoint_), size, recv_link, req_in);
 }
 
 Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
@@ -567,6 +576,7 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
   stats_.bytes_ckpt_in += static_cast<double>(got);
   if (role == kRequestData) {
     global_checkpoint_ = hdr;  // version + header; the payload is already in the targets
+    ckpt_header_only_ = true;
     dev_ckpt_->MarkPayloadDelivered();
   }
   stats_.n_device_ckpt_loads += 1;

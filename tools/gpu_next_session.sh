@@ -21,4 +21,8 @@ case ${1:-s8} in
     OUT_NAME=r4_s10 STEPS="robust" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s10 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts" \
       STEPS="gtest" bash tools/gpu_run.sh ;;
+  s11)
+    # the checkpoint-route fix (a device-loaded rank relays on the TCP route), calibration
+    OUT_NAME=r4_s11 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or calibration" \
+      STEPS="gtest" bash tools/gpu_run.sh ;;
 esac
