@@ -221,7 +221,7 @@ class EngineRobust : public EngineBase {
   bool CheckAndRecover(Status s);
   Status TryLoadCheckPoint(bool requester);
   /*! \brief checkpoint load over the device plane (see recovery.cc); kAborted: not applicable */
-  Status TryLoadDeviceCheckPoint(RecoverType role);
+  Status TryLoadDeviceCheckPoint(RecoverType role, bool *used);
   Status TryGetResult(void *buf, size_t size, int seqno, bool requester);
   /*! \brief per-rank role bits of a device recovery transfer, gathered on every rank */
   static constexpr int kReplayCapable = 1, kReplayHolder = 2, kReplayRequester = 4;

@@ -460,8 +460,13 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
                  "LoadCheckPoint: too many nodes failed, cannot recover local state");
   }
   if (device_replay_) {
-    s = TryLoadDeviceCheckPoint(role);
-    if (s != Status::kAborted) return s;  // kAborted here: not applicable, use the TCP route
+    // a failure of the device route (a peer died while it ran) is returned like any other;
+    // only a route that does not apply falls through to TCP -- falling through on a failure
+    // would materialise the holders' HBM snapshots for a route the dead peer breaks anyway,
+    // leaving the retry without device holders
+    bool used = false;
+    s = TryLoadDeviceCheckPoint(role, &used);
+    if (s != Status::kSuccess || used) return s;
   }
   // A rank that loaded this version over the device route keeps only its header: the payload
   // went into the caller's tensors, which the caller has changed since.  On the TCP route it
@@ -490,12 +495,13 @@ Status EngineRobust::TryLoadCheckPoint(bool requester) {
   return TryRecoverData(tcp_role, BeginPtr(global_checkpoint_), size, recv_link, req_in);
 }
 
-Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
+Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role, bool *used) {
   // A device checkpoint (HBM snapshot) on the holders and an HBM loader on the requesters: the
   // lowest holder broadcasts the small header over the TCP tree, and every requester copies
   // the buffers from one holder's snapshot (one xGMI hop, holders taken in turn) instead of
   // serialising the model through host memory; the other ranks move no payload.  Every rank
-  // runs the agreement round; kAborted (with no side effect) means "take the TCP route".
+  // runs the agreement round; *used = false (with no side effect) means "take the TCP route",
+  // any other outcome is the route's own status.
   const bool holder_dev = role == kHaveData && global_lazycheck_ != nullptr && dev_ckpt_ &&
                           dev_ckpt_->IsSnapshot(global_lazycheck_);
   const bool req_dev = role == kRequestData && dev_ckpt_ && dev_ckpt_->loader_active();
@@ -512,7 +518,8 @@ Status EngineRobust::TryLoadDeviceCheckPoint(RecoverType role) {
     if (code[r] & kReplayHolder) holders.push_back(r);
     if (code[r] & kReplayRequester) requesters.push_back(r);
   }
-  if (!capable || holders.empty()) return Status::kAborted;
+  *used = capable && !holders.empty();
+  if (!*used) return Status::kSuccess;
   device::DeviceGuard dg(dev_->device());
   const int root = holders[0];
   std::string hdr;

@@ -25,4 +25,10 @@ case ${1:-s8} in
     # the checkpoint-route fix (a device-loaded rank relays on the TCP route), calibration
     OUT_NAME=r4_s11 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or calibration" \
       STEPS="gtest" bash tools/gpu_run.sh ;;
+  s12a)
+    OUT_NAME=r4_s12a GPU_FILES="tests/test_bench_contract.py tests/test_gpu_device_reducer.py tests/test_gpu_engine.py tests/test_gpu_kernels.py tests/test_gpu_models.py" \
+      STEPS="gfiles smoke bench1 prof" bash tools/gpu_run.sh ;;
+  s12b)
+    OUT_NAME=r4_s12b GPU_FILES="tests/test_gpu_multirank.py tests/test_gpu_rccl_lifecycle.py tests/test_gpu_recovery.py tests/test_recovery.py" \
+      STEPS="gfiles shared" bash tools/gpu_run.sh ;;
 esac

@@ -10,6 +10,7 @@
 # Steps:
 #   tests     pytest -m gpu (whole GPU suite, one process)
 #   gtest     pytest -m gpu -k "$GPU_K" (a subset)
+#   gfiles    pytest -m gpu over the files $GPU_FILES (the suite split over two calls)
 #   smoke     __graft_entry__.smoke()
 #   bench1    bench.py at N=1 (the driver's 1-GPU run)
 #   shared    the driver's N = $SHARED_NS launches (torchrun, every rank on this box's one GPU)
@@ -40,6 +41,7 @@ for s in ${STEPS:-tests smoke bench1}; do
   case $s in
     tests)  step pytest_gpu 1100 $PYT tests -m gpu ;;
     gtest)  step pytest_gpu_k 900 $PYT tests -m gpu -k "${GPU_K:?set GPU_K}" ;;
+    gfiles) step pytest_gpu_files 1000 $PYT ${GPU_FILES:?set GPU_FILES} -m gpu ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1) step bench_n1 300 python bench.py --steps ${STEPS_K:-20} --warmup 5 ;;
     shared)
