@@ -36,7 +36,7 @@ step() {
   tail -3 "$OUT/$name.log"
   if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.log"; echo "stopping: $name rc=$rc"; exit $rc; fi
 }
-PYT="python -u -m pytest -x -q -s -p no:cacheprovider --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -x -q -s -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25"
 for s in ${STEPS:-tests smoke bench1}; do
   case $s in
     tests)  step pytest_gpu 1100 $PYT tests -m gpu ;;
