@@ -744,6 +744,12 @@ def main():
                       "fused_chunks": st.get("fused_chunks", 0),
                       "calibration_heap_inputs": bool(st.get("calib_heap_src", 0)),
                       "peer_links": st.get("peer_links"),
+                      # HBM free at start-up (every process on this GPU counted) and the result
+                      # log reserved from it: a log that outgrows its reserve allocates or
+                      # spills inside the timed loop
+                      "free_hbm_at_start_GiB": round(free_hbm / 2 ** 30, 1),
+                      "log_reserve_GiB": round(int(log["rabit_device_log_reserve"]) / 2 ** 30, 2),
+                      "log_spilled_results": st.get("n_spilled_results", 0),
                       "rccl_tuning": st.get("rccl_tuning")},
         "variants": None,
         "direct_phase_breakdown": None,

@@ -31,4 +31,29 @@ case ${1:-s8} in
   s12b)
     OUT_NAME=r4_s12b GPU_FILES="tests/test_gpu_multirank.py tests/test_gpu_rccl_lifecycle.py tests/test_gpu_recovery.py tests/test_recovery.py" \
       STEPS="gfiles shared" bash tools/gpu_run.sh ;;
+  s13)
+    # a slow headline after the suite: what holds the GPU after the hang tests?
+    timeout -k 10 120 python tools/hbm_probe.py start || exit $?
+    OUT_NAME=r4_s13 GPU_K="device_hang_detected" STEPS="gtest" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py after_hang_tests || exit $?
+    sleep 5
+    timeout -k 10 120 python tools/hbm_probe.py after_5s || exit $?
+    OUT_NAME=r4_s13 SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py end ;;
+  s14)
+    # the multirank tests s7b did not run (s8's benches after s7b were fine, s12b's after the
+    # whole file were not), then what holds the GPU, then the N=2 bench
+    OUT_NAME=r4_s14 GPU_FILES="tests/test_gpu_multirank.py" GPU_K="not (calibration_flow or symmetric_zero_copy or registered_zero_copy or gradient_buckets or bench_torchrun_shared_gpu or direct_half_precision or device_local_checkpoint_recovery or device_hang_detected or forced_rccl_on_shared or rccl_init_failure_falls_back or small_op_stress)" \
+      STEPS="gtestf" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py after_tests || exit $?
+    OUT_NAME=r4_s14 SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py end ;;
+  s15)
+    # the rest of s12b's set (s14 ran the first part): multirank tests s7b also ran, RCCL
+    # lifecycle, recovery; then what holds the GPU, then the N=2 bench
+    OUT_NAME=r4_s15 GPU_FILES="tests/test_gpu_multirank.py tests/test_gpu_rccl_lifecycle.py tests/test_gpu_recovery.py tests/test_recovery.py" GPU_K="calibration_flow or symmetric_zero_copy or registered_zero_copy or gradient_buckets or bench_torchrun_shared_gpu or direct_half_precision or device_local_checkpoint_recovery or device_hang_detected or forced_rccl_on_shared or rccl_init_failure_falls_back or small_op_stress or rccl_lifecycle or test_gpu_recovery or test_recovery" \
+      STEPS="gtestf" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py after_tests || exit $?
+    OUT_NAME=r4_s15 SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh || exit $?
+    timeout -k 10 120 python tools/hbm_probe.py end ;;
 esac

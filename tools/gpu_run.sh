@@ -42,6 +42,7 @@ for s in ${STEPS:-tests smoke bench1}; do
     tests)  step pytest_gpu 1100 $PYT tests -m gpu ;;
     gtest)  step pytest_gpu_k 900 $PYT tests -m gpu -k "${GPU_K:?set GPU_K}" ;;
     gfiles) step pytest_gpu_files 1000 $PYT ${GPU_FILES:?set GPU_FILES} -m gpu ;;
+    gtestf) step pytest_gpu_fk 1000 $PYT ${GPU_FILES:?set GPU_FILES} -m gpu -k "${GPU_K:?set GPU_K}" ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1) step bench_n1 300 python bench.py --steps ${STEPS_K:-20} --warmup 5 ;;
     shared)
