@@ -837,6 +837,7 @@ Status DevicePlane::WaitUntil(const Poll &poll, const FailureProbe &probe) {
                              why == 1   ? "abort raised"
                              : why == 2 ? "a zero-copy source was not mapped"
                              : why == 3 ? "deadline"
+                             : why == 4 ? "a peer aborted the group"
                                         : "unknown",
                              RegistryJson().c_str());
         if (force_ == 1) {

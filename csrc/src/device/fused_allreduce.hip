@@ -123,7 +123,8 @@ __device__ __forceinline__ bool Await(const FusedAllreduceArgs &a, int *s_bad, i
       if (f != nullptr) {
         const long long t0 = wall_clock64();
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
-          if (*a.abort_word != 0 || wall_clock64() - t0 > a.deadline_ticks || GroupFailed(a)) {
+          if (*a.abort_word != 0 || *a.peer_abort != 0 || wall_clock64() - t0 > a.deadline_ticks ||
+              GroupFailed(a)) {
             ok = false;
             break;
           }

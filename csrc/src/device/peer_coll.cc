@@ -118,6 +118,8 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
            "hipHostMalloc(peer words)");
   host_words_ = static_cast<int *>(hw);
   std::memset(host_words_, 0, 64);
+  // its own stream: an abort is signalled while the group's stream is blocked in a barrier
+  CheckHip(hipStreamCreateWithFlags(&abort_stream_, hipStreamNonBlocking), "abort stream");
   CheckHip(hipDeviceGetAttribute(&clock_khz_, hipDeviceAttributeWallClockRate, device_),
            "wall clock");
   set_deadline_sec(deadline_sec);
@@ -140,6 +142,10 @@ PeerGroup::~PeerGroup() {
   }
   if (table_ != nullptr) (void)hipFree(const_cast<void **>(table_));
   if (meta_table_ != nullptr) (void)hipFree(meta_table_);
+  if (abort_stream_ != nullptr) {
+    (void)hipStreamSynchronize(abort_stream_);
+    (void)hipStreamDestroy(abort_stream_);
+  }
   if (base_ != nullptr) (void)hipFree(base_);
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
 }
@@ -239,6 +245,18 @@ char *PeerGroup::stage(int rank, int which) const {
 void PeerGroup::SignalAbort() {
   if (host_words_ != nullptr) {
     __atomic_store_n(&host_words_[0], 1, __ATOMIC_SEQ_CST);
+  }
+  // every peer's barriers and fused waits give up too (kPeerAbortOffset): a dead rank is seen
+  // first by the ranks whose links it closed, and this carries it to the others over xGMI
+  // instead of their own TCP links (once per group; best effort: a failed write only leaves a
+  // peer to find the failure itself)
+  if (!opened_ || abort_stream_ == nullptr || peers_signalled_.exchange(true)) return;
+  for (int p = 0; p < n_; ++p) {
+    if (p == rank_ || peer_base_[p] == nullptr) continue;
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(peer_base_[p] + kPeerAbortOffset), 1,
+                          1, abort_stream_) != hipSuccess) {
+      (void)hipGetLastError();
+    }
   }
 }
 
@@ -396,6 +414,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.alpha = alpha;
       fa.post = post_scale ? alpha : 0.0;
       fa.abort_word = &host_words_[0];
+      fa.peer_abort = peer_abort();
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;
@@ -438,6 +457,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.alpha = alpha;
       fa.post = post_scale ? alpha : 0.0;
       fa.abort_word = &host_words_[0];
+      fa.peer_abort = peer_abort();
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;

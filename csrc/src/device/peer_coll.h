@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "device/peer_registry.h"
@@ -52,6 +53,13 @@ constexpr size_t kPeerFlagBytes = 64 * 1024;
 /*! \brief exit status of a rank leaving through the mock_die_mid hook (the launcher restarts it) */
 constexpr int kMockDieMidExitCode = 250;
 constexpr size_t kPeerStatusOffset = 4096;
+/*! \brief an int that peers raise when they abort the group: PeerGroup::SignalAbort writes it into
+ *  every peer's flag area over the IPC mappings, and every barrier and fused wait polls its own
+ *  copy next to the host abort word.  The rank that sees a failure first (a dead peer's sockets
+ *  closing) so ends every rank's spinning kernels at once, instead of each rank waiting to learn
+ *  of it on its own TCP links.  A group stays failed after an abort and the next epoch builds a
+ *  new, zeroed one, so the word needs no reset */
+constexpr size_t kPeerAbortOffset = kPeerStatusOffset + 1024;
 /*! \brief two mailbox words (by stage parity): where this rank's input of the current chunk
  *  lives, published before the first barrier of the chunk (see ResolveArgs) */
 constexpr size_t kPeerMailboxOffset = 8192;
@@ -164,6 +172,7 @@ struct FusedAllreduceArgs {
   int dtype, op, prep;
   double alpha, post;
   const volatile int *abort_word;
+  const volatile int *peer_abort;  // this rank's copy of the peers' abort word (kPeerAbortOffset)
   int *dev_status, *host_status;
   long long deadline_ticks;
   // optional completion signal (fused one-shot): every workgroup counts itself in on done_count
@@ -324,7 +333,8 @@ class PeerGroup {
   void SignalAbort();
   /*! \brief true when a barrier gave up (read after the stream drained) */
   bool failed() const;
-  /*! \brief why the group failed: 1 abort word, 2 unmapped zero-copy source, 3 deadline */
+  /*! \brief why the group failed: 1 abort word, 2 unmapped zero-copy source, 3 deadline,
+   *         4 a peer aborted the group */
   int fail_reason() const {
     return host_words_ != nullptr ? __atomic_load_n(&host_words_[1], __ATOMIC_SEQ_CST) : 0;
   }
@@ -446,6 +456,7 @@ class PeerGroup {
                                                   static_cast<size_t>(which) * fused_block_bytes_);
   }
   int *dev_status() const { return reinterpret_cast<int *>(base_ + kPeerStatusOffset); }
+  int *peer_abort() const { return reinterpret_cast<int *>(base_ + kPeerAbortOffset); }
   unsigned int *done_count() const {
     return reinterpret_cast<unsigned int *>(base_ + kPeerStatusOffset + 256);
   }
@@ -475,6 +486,8 @@ class PeerGroup {
   std::vector<char *> peer_heap_;       // mapped heaps (own = heap_.base), nullptr if none
   const void **table_{nullptr};         // device table of resolved reduce sources
   int *host_words_{nullptr};            // pinned: [0] abort, [1] status
+  hipStream_t abort_stream_{nullptr};   // SignalAbort's writes into the peers' flag areas
+  std::atomic<bool> peers_signalled_{false};
   int n_{0}, rank_{0};
   unsigned long long epoch_{0};
   int parity_{0};

@@ -83,14 +83,18 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
   }
   // make the bytes written by earlier kernels of this stream visible before signalling
   __threadfence_system();
+  // raised by a peer that aborted the group (kPeerAbortOffset of this rank's own flag area)
+  const volatile int *peer_abort = reinterpret_cast<const volatile int *>(
+      reinterpret_cast<const char *>(flags.p[rank]) + kPeerAbortOffset);
   if (t < n) {
     __hip_atomic_store(flags.p[t] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned long long *mine = flags.p[rank] + t;
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      if (*abort_word != 0 || wall_clock64() - t0 > deadline_ticks) {
-        // the reason, for the host's log: 1 the host raised the abort word, 3 the deadline
-        const int why = *abort_word != 0 ? 1 : 3;
+      if (*abort_word != 0 || *peer_abort != 0 || wall_clock64() - t0 > deadline_ticks) {
+        // the reason, for the host's log: 1 the host raised the abort word, 4 a peer aborted
+        // the group, 3 the deadline
+        const int why = *abort_word != 0 ? 1 : (*peer_abort != 0 ? 4 : 3);
         __hip_atomic_store(dev_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;

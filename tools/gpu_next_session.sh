@@ -56,4 +56,13 @@ case ${1:-s8} in
     timeout -k 10 120 python tools/hbm_probe.py after_tests || exit $?
     OUT_NAME=r4_s15 SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh || exit $?
     timeout -k 10 120 python tools/hbm_probe.py end ;;
+  s16)
+    # the bench with a checkpoint before its timed loop; the bench's own GPU tests
+    OUT_NAME=r4_s16 GPU_K="bench" STEPS="gtest smoke bench1 shared" bash tools/gpu_run.sh ;;
+  s17)
+    # peers' barriers poisoned by the rank that sees a failure first (kPeerAbortOffset): the
+    # recovery breakdown, then the fault-tolerance GPU tests
+    OUT_NAME=r4_s17 STEPS="robust" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s17 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or calibration or direct_collectives" \
+      STEPS="gtest" bash tools/gpu_run.sh ;;
 esac
