@@ -730,6 +730,7 @@ bool DevicePlane::PreparePeers(PeerRecord *rec, std::string *why) {
     peers_->set_fused_oneshot_max(cfg_.fused_oneshot_max);
     peers_->set_fused_min_bytes(cfg_.fused_min_bytes);
     peers_->set_done_signal(cfg_.done_word);
+    peers_->set_peer_abort(cfg_.peer_abort);
     peers_->set_bcast_chunk(cfg_.bcast_chunk);
     // pipelined push form: forced on (with push), or off until the calibration decides
     peers_->set_pipeline(cfg_.pipeline_mode == 1);
@@ -861,7 +862,10 @@ Status DevicePlane::WaitUntil(const Poll &poll, const FailureProbe &probe) {
       }
     }
     const double waited = std::chrono::duration<double>(clock::now() - t0).count();
-    if (probe && (iter & 63) == 0 && waited > 1e-3 && probe()) {
+    // the host's view of the peers (their links), about once a millisecond once the op has
+    // waited that long: the rank that notices a death first aborts every rank's kernels
+    // (PeerGroup::SignalAbort), so this interval is most of the job's detection latency
+    if (probe && (iter & 15) == 0 && waited > 1e-3 && probe()) {
       AbortComm();  // drains the stream, or ends the process if this rank's work is wedged
       return Status::kAborted;
     }

@@ -91,6 +91,8 @@ struct DeviceConfig {
   // of every channel) runs on a helper thread watched by the failure probe and a deadline, so
   // a peer that dies mid-init costs kAborted / kTimeout instead of a hang (see InitComm)
   double comm_init_timeout_sec{120};   // deadline of communicator bring-up (0: none)
+  bool peer_abort{true};               // an abort raises the peers' abort words too
+                                       // (rabit_device_peer_abort, PeerGroup::SignalAbort)
   bool done_word{true};                // small direct ops: poll a kernel-written host word for
                                        // completion instead of an event
   int rccl_max_failures{8};            // consecutive aborted RCCL ops before the error is fatal

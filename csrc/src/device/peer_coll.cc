@@ -118,8 +118,6 @@ PeerGroup::PeerGroup(int device, size_t stage_bytes, double deadline_sec, hipStr
            "hipHostMalloc(peer words)");
   host_words_ = static_cast<int *>(hw);
   std::memset(host_words_, 0, 64);
-  // its own stream: an abort is signalled while the group's stream is blocked in a barrier
-  CheckHip(hipStreamCreateWithFlags(&abort_stream_, hipStreamNonBlocking), "abort stream");
   CheckHip(hipDeviceGetAttribute(&clock_khz_, hipDeviceAttributeWallClockRate, device_),
            "wall clock");
   set_deadline_sec(deadline_sec);
@@ -242,6 +240,14 @@ char *PeerGroup::stage(int rank, int which) const {
          static_cast<size_t>(which) * stage_bytes_;
 }
 
+void PeerGroup::set_peer_abort(bool on) {
+  peer_abort_ = on;
+  // its own stream: an abort is signalled while the group's stream is blocked in a barrier
+  if (on && abort_stream_ == nullptr) {
+    CheckHip(hipStreamCreateWithFlags(&abort_stream_, hipStreamNonBlocking), "abort stream");
+  }
+}
+
 void PeerGroup::SignalAbort() {
   if (host_words_ != nullptr) {
     __atomic_store_n(&host_words_[0], 1, __ATOMIC_SEQ_CST);
@@ -250,7 +256,9 @@ void PeerGroup::SignalAbort() {
   // first by the ranks whose links it closed, and this carries it to the others over xGMI
   // instead of their own TCP links (once per group; best effort: a failed write only leaves a
   // peer to find the failure itself)
-  if (!opened_ || abort_stream_ == nullptr || peers_signalled_.exchange(true)) return;
+  if (!peer_abort_ || !opened_ || abort_stream_ == nullptr || peers_signalled_.exchange(true)) {
+    return;
+  }
   for (int p = 0; p < n_; ++p) {
     if (p == rank_ || peer_base_[p] == nullptr) continue;
     if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(peer_base_[p] + kPeerAbortOffset), 1,

@@ -414,6 +414,8 @@ class PeerGroup {
     *epoch = done_epoch_;
     return true;
   }
+  /*! \brief an abort also raises every peer's abort word (rabit_device_peer_abort) */
+  void set_peer_abort(bool on);
   /*! \brief polling the done word instead of an event (rabit_device_done_word) */
   void set_done_signal(bool v) { done_signal_ = v; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
@@ -488,6 +490,7 @@ class PeerGroup {
   int *host_words_{nullptr};            // pinned: [0] abort, [1] status
   hipStream_t abort_stream_{nullptr};   // SignalAbort's writes into the peers' flag areas
   std::atomic<bool> peers_signalled_{false};
+  bool peer_abort_{false};
   int n_{0}, rank_{0};
   unsigned long long epoch_{0};
   int parity_{0};

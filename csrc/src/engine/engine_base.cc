@@ -128,6 +128,7 @@ void EngineBase::SetParam(const char *name, const char *val) {
   if (is("rabit_rccl_max_failures")) dcfg_.rccl_max_failures = atoi(val);
   if (is("rabit_mock_rccl_error")) dcfg_.mock_rccl_error = atoi(val);
   if (is("rabit_device_done_word")) dcfg_.done_word = utils::StringToBool(val);
+  if (is("rabit_device_peer_abort")) dcfg_.peer_abort = utils::StringToBool(val);
   if (is("rabit_rccl_tune_ctas")) rccl_tune_ctas_ = val;
   if (is("rabit_device_fused_min")) dcfg_.fused_min_bytes = core::ParseUnit(name, val);
   if (is("rabit_device_direct_mode")) {

@@ -65,4 +65,12 @@ case ${1:-s8} in
     OUT_NAME=r4_s17 STEPS="robust" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s17 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or calibration or direct_collectives" \
       STEPS="gtest" bash tools/gpu_run.sh ;;
+  s18)
+    # the recovery breakdown, three kill runs (eight ranks time-slicing one GPU vary run to run)
+    OUT_NAME=r4_s18 ROBUST_REPS=3 STEPS="robust" bash tools/gpu_run.sh ;;
+  s19)
+    # A/B on one box: the peer abort on (default) and off, three kill runs each
+    OUT_NAME=r4_s19 ROBUST_REPS=3 STEPS="robust" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s19_nopa ROBUST_REPS=3 ROBUST_ARGS="rabit_device_peer_abort=0" STEPS="robust" \
+      bash tools/gpu_run.sh ;;
 esac

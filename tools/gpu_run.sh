@@ -17,7 +17,8 @@
 #   prof      rocprofv3 --kernel-trace --stats of the N=1 bench
 #   kbench    kernel bench against the measured HBM peak
 #   robust    tools/robust_bench.py = BASELINE config 5 on $ROBUST_N (8) shared ranks: clean, then
-#             rank 3 killed at version 4 (restarted by the launcher), recovery phase breakdown
+#             rank 3 killed at version 4 (restarted by the launcher), recovery phase breakdown;
+#             ROBUST_REPS=k repeats the kill run (robust_kill_<i>.log)
 #   zctrace   tools/zero_copy_trace.sh: kernel order with / without the zero-copy registry
 #   cmd       an arbitrary command: CMD="..." (limit CMD_LIMIT seconds, default 300)
 set -u
@@ -57,9 +58,12 @@ for s in ${STEPS:-tests smoke bench1}; do
     robust)
       step robust_clean 260 env XR_ITERS=12 python -m rabit_amd.launcher -n ${ROBUST_N:-8} \
         --num-attempt 1 --timeout 240 -- python -u tools/robust_bench.py ${ROBUST_ARGS:-}
-      step robust_kill 260 env XR_ITERS=12 python -m rabit_amd.launcher -n ${ROBUST_N:-8} \
-        --num-attempt 2 --timeout 240 -- python -u tools/robust_bench.py mock=3,4,0,0 \
-        ${ROBUST_ARGS:-} ;;
+      for rep in $(seq 1 ${ROBUST_REPS:-1}); do
+        sfx=$([ "${ROBUST_REPS:-1}" = 1 ] || echo "_$rep")
+        step robust_kill$sfx 260 env XR_ITERS=12 python -m rabit_amd.launcher -n ${ROBUST_N:-8} \
+          --num-attempt 2 --timeout 240 -- python -u tools/robust_bench.py mock=3,4,0,0 \
+          ${ROBUST_ARGS:-}
+      done ;;
     zctrace) step zctrace 300 bash tools/zero_copy_trace.sh ;;
     cmd)    step cmd 600 bash -c "${CMD:?set CMD}" ;;
     *) echo "unknown step $s"; exit 2 ;;
