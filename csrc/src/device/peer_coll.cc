@@ -140,10 +140,6 @@ PeerGroup::~PeerGroup() {
   }
   if (table_ != nullptr) (void)hipFree(const_cast<void **>(table_));
   if (meta_table_ != nullptr) (void)hipFree(meta_table_);
-  if (abort_stream_ != nullptr) {
-    (void)hipStreamSynchronize(abort_stream_);
-    (void)hipStreamDestroy(abort_stream_);
-  }
   if (base_ != nullptr) (void)hipFree(base_);
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
 }
@@ -240,32 +236,11 @@ char *PeerGroup::stage(int rank, int which) const {
          static_cast<size_t>(which) * stage_bytes_;
 }
 
-void PeerGroup::set_peer_abort(bool on) {
-  peer_abort_ = on;
-  // its own stream: an abort is signalled while the group's stream is blocked in a barrier
-  if (on && abort_stream_ == nullptr) {
-    CheckHip(hipStreamCreateWithFlags(&abort_stream_, hipStreamNonBlocking), "abort stream");
-  }
-}
-
 void PeerGroup::SignalAbort() {
   if (host_words_ != nullptr) {
     __atomic_store_n(&host_words_[0], 1, __ATOMIC_SEQ_CST);
   }
-  // every peer's barriers and fused waits give up too (kPeerAbortOffset): a dead rank is seen
-  // first by the ranks whose links it closed, and this carries it to the others over xGMI
-  // instead of their own TCP links (once per group; best effort: a failed write only leaves a
-  // peer to find the failure itself)
-  if (!peer_abort_ || !opened_ || abort_stream_ == nullptr || peers_signalled_.exchange(true)) {
-    return;
-  }
-  for (int p = 0; p < n_; ++p) {
-    if (p == rank_ || peer_base_[p] == nullptr) continue;
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(peer_base_[p] + kPeerAbortOffset), 1,
-                          1, abort_stream_) != hipSuccess) {
-      (void)hipGetLastError();
-    }
-  }
+  // (a barrier kernel that sees this word passes the abort on to every peer: kPeerAbortOffset)
 }
 
 bool PeerGroup::failed() const {
@@ -279,7 +254,7 @@ hipError_t PeerGroup::Barrier(const ResolveArgs *resolve) {
   }
   ++epoch_;  // (statistics: the barrier's number itself lives in barrier_counter())
   return LaunchPeerBarrier(t, rank_, n_, barrier_counter(), &host_words_[0], dev_status(),
-                           &host_words_[1], deadline_ticks_, resolve, stream_);
+                           &host_words_[1], deadline_ticks_, peer_abort_ ? 1 : 0, resolve, stream_);
 }
 
 #define XRABIT_TRY_HIP(expr)              \
@@ -422,7 +397,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.alpha = alpha;
       fa.post = post_scale ? alpha : 0.0;
       fa.abort_word = &host_words_[0];
-      fa.peer_abort = peer_abort();
+      fa.peer_abort = peer_abort_ ? peer_abort() : &host_words_[0];
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;
@@ -465,7 +440,7 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
       fa.alpha = alpha;
       fa.post = post_scale ? alpha : 0.0;
       fa.abort_word = &host_words_[0];
-      fa.peer_abort = peer_abort();
+      fa.peer_abort = peer_abort_ ? peer_abort() : &host_words_[0];
       fa.dev_status = dev_status();
       fa.host_status = &host_words_[1];
       fa.deadline_ticks = deadline_ticks_;

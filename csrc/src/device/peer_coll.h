@@ -53,12 +53,15 @@ constexpr size_t kPeerFlagBytes = 64 * 1024;
 /*! \brief exit status of a rank leaving through the mock_die_mid hook (the launcher restarts it) */
 constexpr int kMockDieMidExitCode = 250;
 constexpr size_t kPeerStatusOffset = 4096;
-/*! \brief an int that peers raise when they abort the group: PeerGroup::SignalAbort writes it into
- *  every peer's flag area over the IPC mappings, and every barrier and fused wait polls its own
- *  copy next to the host abort word.  The rank that sees a failure first (a dead peer's sockets
- *  closing) so ends every rank's spinning kernels at once, instead of each rank waiting to learn
- *  of it on its own TCP links.  A group stays failed after an abort and the next epoch builds a
- *  new, zeroed one, so the word needs no reset */
+/*! \brief an int that peers raise when they give up on the group: a barrier kernel that gives up
+ *  on its own account (the host raised the abort word: it saw a failure, e.g. a dead peer's
+ *  sockets closing; or the deadline passed) stores it into every peer's flag area over the IPC
+ *  mappings, and every barrier and fused wait polls its own copy next to the host abort word.
+ *  The rank that sees a failure first so ends every rank's spinning kernels at once, instead of
+ *  each rank waiting to learn of it on its own TCP links.  No stream and no host call is involved
+ *  (a HIP stream per group cost tens of ms of bring-up with 8 ranks on one GPU,
+ *  profiles/r4_recovery/).  A group stays failed after an abort and the next epoch builds a new,
+ *  zeroed one, so the word needs no reset */
 constexpr size_t kPeerAbortOffset = kPeerStatusOffset + 1024;
 /*! \brief two mailbox words (by stage parity): where this rank's input of the current chunk
  *  lives, published before the first barrier of the chunk (see ResolveArgs) */
@@ -203,7 +206,7 @@ hipError_t LaunchFusedOneshot(const FusedAllreduceArgs &args, int grid, hipStrea
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n,
                              unsigned long long *counter, const volatile int *abort_word,
                              int *dev_status, int *host_status, long long deadline_ticks,
-                             const ResolveArgs *resolve, hipStream_t stream);
+                             int peer_abort_on, const ResolveArgs *resolve, hipStream_t stream);
 hipError_t LaunchCopyBatch(const CopyBatch &batch, hipStream_t stream);
 
 /*! \brief fixed-size record every rank contributes when a group is built */
@@ -415,7 +418,7 @@ class PeerGroup {
     return true;
   }
   /*! \brief an abort also raises every peer's abort word (rabit_device_peer_abort) */
-  void set_peer_abort(bool on);
+  void set_peer_abort(bool on) { peer_abort_ = on; }
   /*! \brief polling the done word instead of an event (rabit_device_done_word) */
   void set_done_signal(bool v) { done_signal_ = v; }
   /*! \brief record hipEvents between the phases of single-chunk allreduces */
@@ -488,9 +491,7 @@ class PeerGroup {
   std::vector<char *> peer_heap_;       // mapped heaps (own = heap_.base), nullptr if none
   const void **table_{nullptr};         // device table of resolved reduce sources
   int *host_words_{nullptr};            // pinned: [0] abort, [1] status
-  hipStream_t abort_stream_{nullptr};   // SignalAbort's writes into the peers' flag areas
-  std::atomic<bool> peers_signalled_{false};
-  bool peer_abort_{false};
+  bool peer_abort_{false};              // rabit_device_peer_abort
   int n_{0}, rank_{0};
   unsigned long long epoch_{0};
   int parity_{0};

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
                                                         const volatile int *abort_word,
                                                         int *dev_status, int *host_status,
                                                         long long deadline_ticks,
-                                                        ResolveArgs resolve) {
+                                                        int peer_abort_on, ResolveArgs resolve) {
   const int t = threadIdx.x;
   // an earlier barrier of this group failed: stay failed, signal nothing
   if (__hip_atomic_load(dev_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
@@ -91,10 +91,20 @@ __global__ __launch_bounds__(64) void PeerBarrierKernel(PeerFlagTable flags, int
     unsigned long long *mine = flags.p[rank] + t;
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      if (*abort_word != 0 || *peer_abort != 0 || wall_clock64() - t0 > deadline_ticks) {
+      if (*abort_word != 0 || (peer_abort_on && *peer_abort != 0) ||
+          wall_clock64() - t0 > deadline_ticks) {
         // the reason, for the host's log: 1 the host raised the abort word, 4 a peer aborted
         // the group, 3 the deadline
-        const int why = *abort_word != 0 ? 1 : (*peer_abort != 0 ? 4 : 3);
+        const int why = *abort_word != 0 ? 1 : (peer_abort_on && *peer_abort != 0 ? 4 : 3);
+        if (peer_abort_on && why != 4) {
+          // this rank gives up on its own account: every peer's waits give up too
+          for (int p = 0; p < n; ++p) {
+            if (p == rank) continue;
+            __hip_atomic_store(reinterpret_cast<int *>(reinterpret_cast<char *>(flags.p[p]) +
+                                                       kPeerAbortOffset),
+                               1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
         __hip_atomic_store(dev_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -336,17 +346,20 @@ hipError_t LaunchAllgatherWindow(const AllgatherWindowArgs &args, hipStream_t st
 hipError_t LaunchPeerBarrier(const PeerFlagTable &flags, int rank, int n,
                              unsigned long long *counter, const volatile int *abort_word,
                              int *dev_status, int *host_status, long long deadline_ticks,
+                             int peer_abort_on,
                              const ResolveArgs *resolve, hipStream_t stream) {
   if (n < 1 || n > kMaxPeers || rank < 0 || rank >= n || counter == nullptr) {
     return hipErrorInvalidValue;
   }
   if (resolve != nullptr) {
     hipLaunchKernelGGL(PeerBarrierKernel<true>, dim3(1), dim3(64), 0, stream, flags, rank, n,
-                       counter, abort_word, dev_status, host_status, deadline_ticks, *resolve);
+                       counter, abort_word, dev_status, host_status, deadline_ticks, peer_abort_on,
+                       *resolve);
   } else {
     ResolveArgs none{};
     hipLaunchKernelGGL(PeerBarrierKernel<false>, dim3(1), dim3(64), 0, stream, flags, rank, n,
-                       counter, abort_word, dev_status, host_status, deadline_ticks, none);
+                       counter, abort_word, dev_status, host_status, deadline_ticks, peer_abort_on,
+                       none);
   }
   return hipGetLastError();
 }

@@ -73,4 +73,9 @@ case ${1:-s8} in
     OUT_NAME=r4_s19 ROBUST_REPS=3 STEPS="robust" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s19_nopa ROBUST_REPS=3 ROBUST_ARGS="rabit_device_peer_abort=0" STEPS="robust" \
       bash tools/gpu_run.sh ;;
+  s20)
+    # A/B again with the abort passed on by the barrier kernel itself (no stream per group)
+    OUT_NAME=r4_s20 ROBUST_REPS=3 STEPS="robust" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_s20_nopa ROBUST_REPS=3 ROBUST_ARGS="rabit_device_peer_abort=0" STEPS="robust" \
+      bash tools/gpu_run.sh ;;
 esac
