@@ -78,4 +78,10 @@ case ${1:-s8} in
     OUT_NAME=r4_s20 ROBUST_REPS=3 STEPS="robust" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_s20_nopa ROBUST_REPS=3 ROBUST_ARGS="rabit_device_peer_abort=0" STEPS="robust" \
       bash tools/gpu_run.sh ;;
+  s21a)
+    OUT_NAME=r4_s21a GPU_FILES="tests/test_bench_contract.py tests/test_gpu_device_reducer.py tests/test_gpu_engine.py tests/test_gpu_kernels.py tests/test_gpu_models.py" \
+      STEPS="gfiles smoke bench1 prof" bash tools/gpu_run.sh ;;
+  s21b)
+    OUT_NAME=r4_s21b GPU_FILES="tests/test_gpu_multirank.py tests/test_gpu_rccl_lifecycle.py tests/test_gpu_recovery.py tests/test_recovery.py" \
+      STEPS="gfiles shared" bash tools/gpu_run.sh ;;
 esac
