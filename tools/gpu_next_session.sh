@@ -84,4 +84,8 @@ case ${1:-s8} in
   s21b)
     OUT_NAME=r4_s21b GPU_FILES="tests/test_gpu_multirank.py tests/test_gpu_rccl_lifecycle.py tests/test_gpu_recovery.py tests/test_recovery.py" \
       STEPS="gfiles shared" bash tools/gpu_run.sh ;;
+  s22)
+    # ExitProcess without allocation: the fault-tolerance GPU tests and one config-5 kill run
+    OUT_NAME=r4_s22 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or rccl_lifecycle or test_recovery" \
+      STEPS="gtest robust" bash tools/gpu_run.sh ;;
 esac
