@@ -88,4 +88,7 @@ case ${1:-s8} in
     # ExitProcess without allocation: the fault-tolerance GPU tests and one config-5 kill run
     OUT_NAME=r4_s22 GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or rccl_lifecycle or test_recovery" \
       STEPS="gtest robust" bash tools/gpu_run.sh ;;
+  s23)
+    # the whole GPU suite in one call, as the driver runs it at round end, then smoke
+    OUT_NAME=r4_s23 STEPS="tests smoke" bash tools/gpu_run.sh ;;
 esac
