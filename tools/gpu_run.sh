@@ -1,5 +1,6 @@
 #!/bin/bash
-# The one GPU-box session runner (replaces the per-session tools/gpu_r3_s*.sh scripts).
+# The one GPU-box session runner (replaces the per-session scripts of earlier rounds; the named
+# sessions that produced round 4's evidence are in tools/gpu_next_session.sh).
 #
 #   OUT_NAME=r4_xyz STEPS="tests smoke bench1 shared" bash tools/gpu_run.sh
 #
