@@ -309,7 +309,11 @@ hipError_t PeerGroup::AllreduceImpl(const void *send, void *recv, void *recv2, s
   // where it is), so only that form asks for its own input to be exported.
   ++op_seq_;
   const bool registry = registry_ok_ && !no_registry_ && indirect;
-  if (registry) XRABIT_TRY_HIP(registry_.Refresh(op_seq_, stream_));
+  // (a replaced mapping waits for the stream to drain: at most twice the barrier deadline)
+  if (registry) {
+    const double drain_sec = 2.0 * static_cast<double>(deadline_ticks_) / (clock_khz_ * 1e3);
+    XRABIT_TRY_HIP(registry_.Refresh(op_seq_, stream_, drain_sec));
+  }
   unsigned long long reg_mailbox = 0;
   const bool reg_input = registry && zero_copy_min_ != 0 && count * tn >= zero_copy_min_ &&
                          count * tn > oneshot_max_ && !push_ && !fused_ &&

@@ -9,8 +9,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 
 namespace rabit {
 namespace device {
@@ -18,6 +20,21 @@ namespace {
 constexpr uint64_t kRegistryMagic = 0x7872656731ull;  // "xreg1"
 constexpr size_t kPageBytes = (sizeof(RegistryPage) + 4095) / 4096 * 4096;
 constexpr size_t kTableBytes = sizeof(char *) * kMaxRegPeers * kMaxRegs;
+
+/*! \brief wait for `stream` to drain, at most `sec` seconds (a wedged stream must not hang the
+ *  rank here: the op then fails and the engine recovers or restarts the worker) */
+hipError_t Drain(hipStream_t stream, double sec) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(stream);
+    if (e != hipErrorNotReady) return e;
+    if (std::chrono::duration<double>(clock::now() - t0).count() > sec) {
+      return hipErrorLaunchTimeOut;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
 }  // namespace
 
 PeerRegistry::~PeerRegistry() {
@@ -117,7 +134,7 @@ void PeerRegistry::Seal() {
   sealed_ = true;
 }
 
-hipError_t PeerRegistry::Refresh(uint64_t op, hipStream_t stream) {
+hipError_t PeerRegistry::Refresh(uint64_t op, hipStream_t stream, double drain_sec) {
   if (!opened_) return hipSuccess;
   bool dirty = false, drained = false;
   struct PendingAck {
@@ -150,7 +167,7 @@ hipError_t PeerRegistry::Refresh(uint64_t op, hipStream_t stream) {
       if (mapped_[q][k] != nullptr) {
         // an op already enqueued may still read through the old mapping: drain first
         if (!drained) {
-          hipError_t e = hipStreamSynchronize(stream);
+          hipError_t e = Drain(stream, drain_sec);
           if (e != hipSuccess) return e;
           drained = true;
         }
@@ -169,7 +186,7 @@ hipError_t PeerRegistry::Refresh(uint64_t op, hipStream_t stream) {
           continue;
         }
         if (!drained) {
-          hipError_t e = hipStreamSynchronize(stream);
+          hipError_t e = Drain(stream, drain_sec);
           if (e != hipSuccess) return e;
           drained = true;
         }

@@ -91,9 +91,11 @@ class PeerRegistry {
   /*!
    * \brief importer side, once per allreduce before its kernels are enqueued (op = this op's
    *        index): map peers' new registrations, update the device table on `stream`, acknowledge.
-   *        hipSuccess or the first HIP error.
+   *        A replaced mapping is closed once `stream` drained, waiting at most `drain_sec`
+   *        (hipErrorLaunchTimeOut after that: the stream is wedged).  hipSuccess or the first
+   *        error.
    */
-  hipError_t Refresh(uint64_t op, hipStream_t stream);
+  hipError_t Refresh(uint64_t op, hipStream_t stream, double drain_sec);
   /*!
    * \brief exporter side: true when [p, p + bytes) may be read in place by every peer in op
    *        `op`; *mailbox then holds the mailbox word of its start.  Registers an allocation

@@ -7,6 +7,7 @@
 #   recovery  config 5 at 8 ranks with the rank-3 kill, 3 runs each with the peer abort on and
 #             off                                                               -> r4_recovery/
 #   ft        the fault-tolerance GPU tests (chaos, recovery, hangs, kills, RCCL lifecycle)
+#   zc        the zero-copy and allgather GPU tests, then the N=2 launch
 set -u
 case ${1:-final} in
   final) OUT_NAME=r4_final_suite STEPS="tests smoke" bash tools/gpu_run.sh ;;
@@ -24,5 +25,9 @@ case ${1:-final} in
   ft)
     OUT_NAME=r4_ft GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or rccl_lifecycle or test_recovery" \
       STEPS="gtest" bash tools/gpu_run.sh ;;
+  zc)
+    OUT_NAME=r4_zc GPU_K="zero_copy or symmetric or allgather_layout or calibration_flow" \
+      STEPS="gtest" bash tools/gpu_run.sh || exit $?
+    OUT_NAME=r4_zc SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
