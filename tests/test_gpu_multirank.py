@@ -233,6 +233,18 @@ def test_registered_zero_copy(world, args):
     assert out.count("ZEROCOPY OK") == world, out[-3000:]
 
 
+def test_registered_zero_copy_expandable_segments():
+    """torch's expandable segments are VMM allocations: inputs the registry cannot export are
+    staged (the fallback the registry promises), mapped ones read in place; exact either way"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rc, out = _run("zero_copy_check.py", 2, [],
+                   env={"PYTORCH_HIP_ALLOC_CONF": "expandable_segments:True"})
+    assert rc == 0, out[-5000:]
+    assert out.count("ZEROCOPY OK") == 2, out[-3000:]
+    print([l for l in out.splitlines() if "ZEROCOPY OK" in l][0])
+
+
 @pytest.mark.parametrize("sym", ["0", "1"])
 def test_gradient_buckets(sym):
     if not torch.cuda.is_available():

@@ -26,7 +26,7 @@ case ${1:-final} in
     OUT_NAME=r4_ft GPU_K="chaos or recover or hang or device_ft or mock or kill or adopts or rccl_lifecycle or test_recovery" \
       STEPS="gtest" bash tools/gpu_run.sh ;;
   zc)
-    OUT_NAME=r4_zc GPU_K="zero_copy or symmetric or allgather_layout or calibration_flow" \
+    OUT_NAME=r4_zc GPU_K="zero_copy or symmetric or allgather_layout or calibration_flow or expandable" \
       STEPS="gtest" bash tools/gpu_run.sh || exit $?
     OUT_NAME=r4_zc SHARED_NS=2 STEPS="shared" bash tools/gpu_run.sh ;;
   *) echo "unknown session $1"; exit 2 ;;
