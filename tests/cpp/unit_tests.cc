@@ -23,7 +23,13 @@
 #include <thread>
 #include <vector>
 
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include "coll/host_coll.h"
+#include "core/exit.h"
 #include "core/params.h"
 #include "core/wait_state.h"
 #include "net/link_reset.h"
@@ -102,6 +108,46 @@ void CountTimeout(int, int) { g_timeouts.fetch_add(1); }
 }  // namespace
 
 // ---------------------------------------------------------------- utils / io
+TEST(exit_process_reports_code_and_shuts_sockets) {
+  // a child leaving through ExitProcess (csrc/src/core/exit.h): its exit status is the code, a
+  // peer on a connected socket sees EOF, and the launcher's pipe gets "77\n" -- only when the
+  // XRABIT_EXIT_FD spec names that pipe's inode (a stale spec must write nothing)
+  for (int right_inode = 1; right_inode >= 0; --right_inode) {
+    int pfd[2], sv[2];
+    EXPECT(pipe(pfd) == 0);
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+    struct stat st;
+    EXPECT(fstat(pfd[1], &st) == 0);
+    char spec[64];
+    std::snprintf(spec, sizeof(spec), "%d:%llu", pfd[1],
+                  static_cast<unsigned long long>(st.st_ino) + (right_inode ? 0 : 1));
+    const pid_t pid = fork();
+    if (pid == 0) {
+      close(pfd[0]);
+      close(sv[1]);
+      setenv("XRABIT_EXIT_FD", spec, 1);
+      rabit::utils::ExitProcess(77);
+    }
+    close(pfd[1]);
+    close(sv[0]);
+    char buf[16] = {0};
+    ssize_t got = 0;
+    for (ssize_t k; (k = read(pfd[0], buf + got, sizeof(buf) - 1 - got)) > 0;) got += k;
+    int status = 0;
+    EXPECT(waitpid(pid, &status, 0) == pid);
+    EXPECT(WIFEXITED(status) && WEXITSTATUS(status) == 77);
+    if (right_inode) {
+      EXPECT(got == 3 && std::string(buf) == "77\n");
+    } else {
+      EXPECT(got == 0);
+    }
+    char c;
+    EXPECT(read(sv[1], &c, 1) == 0);
+    close(pfd[0]);
+    close(sv[1]);
+  }
+}
+
 TEST(utils_assert_throws) {
   EXPECT_THROW(rabit::utils::Assert(false, "boom %d", 1));
   EXPECT_THROW(rabit::utils::Check(false, "bad"));
