@@ -174,7 +174,10 @@ def test_allgather_layout_resolved_on_device(world, args):
 # a Max and a 3-chunk broadcast per iteration, then an HBM checkpoint): 1-3 kill points per seed,
 # among them deaths of ranks that serve a replay or a checkpoint load (routing, device exchange)
 # (the seeds with a serving death among the first 15, plus two plain ones)
-DEVICE_CHAOS_SEEDS = [201, 202, 204, 205, 207, 209, 211, 212, 214, 208]
+# the committed seeds; XRABIT_DEVICE_CHAOS_SEEDS="a,b,..." runs others (fuzzing on the GPU box)
+DEVICE_CHAOS_SEEDS = ([int(s) for s in os.environ["XRABIT_DEVICE_CHAOS_SEEDS"].split(",")]
+                      if os.environ.get("XRABIT_DEVICE_CHAOS_SEEDS") else
+                      [201, 202, 204, 205, 207, 209, 211, 212, 214, 208])
 
 
 @pytest.mark.parametrize("seed", DEVICE_CHAOS_SEEDS)
