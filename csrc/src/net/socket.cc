@@ -81,21 +81,30 @@ bool TcpSocket::Connect(const std::string &host, int port) {
   return connect(fd_, reinterpret_cast<sockaddr *>(&addr), sizeof(addr)) == 0;
 }
 
-int TcpSocket::BindRange(int start, int end) {
+int TcpSocket::BindListenRange(int start, int end, int backlog) {
+  // SO_REUSEADDR: a port whose earlier connections linger in TIME_WAIT (a restarted worker's, or
+  // another job's on this host) may be listened on again; without it, many restarts on one host
+  // use the range up 60 s at a time.  Two processes may then both bind a free port, and only
+  // the first listen() succeeds: the other gets EADDRINUSE there and moves on with a new socket
+  // (a bound socket cannot be bound again).
   for (int port = start; port < end; ++port) {
+    if (fd_ < 0) Create();
+    const int one = 1;
+    (void)setsockopt(fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     sockaddr_in addr;
     std::memset(&addr, 0, sizeof(addr));
     addr.sin_family = AF_INET;
     addr.sin_addr.s_addr = htonl(INADDR_ANY);
     addr.sin_port = htons(static_cast<uint16_t>(port));
-    if (bind(fd_, reinterpret_cast<sockaddr *>(&addr), sizeof(addr)) == 0) return port;
-    if (errno != EADDRINUSE && errno != EACCES) break;
+    if (bind(fd_, reinterpret_cast<sockaddr *>(&addr), sizeof(addr)) != 0) {
+      if (errno != EADDRINUSE && errno != EACCES) return -1;
+      continue;  // still unbound: the next port with the same socket
+    }
+    if (listen(fd_, backlog) == 0) return port;
+    if (errno != EADDRINUSE) return -1;
+    Close();
   }
   return -1;
-}
-
-void TcpSocket::Listen(int backlog) {
-  utils::Check(listen(fd_, backlog) == 0, "listen(): %s", strerror(errno));
 }
 
 TcpSocket TcpSocket::Accept() {

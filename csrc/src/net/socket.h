@@ -65,8 +65,8 @@ class TcpSocket {
   /*! \brief blocking connect; false on failure (errno kept) */
   bool Connect(const std::string &host, int port);
   /*! \brief bind to the first free port in [start, end); returns the port or -1 */
-  int BindRange(int start, int end);
-  void Listen(int backlog = 256);
+  /*! \brief listen on the first free port of [start, end): the port, or -1 */
+  int BindListenRange(int start, int end, int backlog = 256);
   TcpSocket Accept();
   void Close();
   bool IsClosed() const { return fd_ < 0; }

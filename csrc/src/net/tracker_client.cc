@@ -73,10 +73,9 @@ void TrackerClient::Relink(const char *cmd, int *rank, int *world_size, Topology
 
   TcpSocket listener;
   listener.Create();
-  int port = listener.BindRange(cfg_->worker_port, cfg_->worker_port + cfg_->nport_trial);
-  utils::Check(port != -1, "cannot bind a worker port in [%d, %d)", cfg_->worker_port,
+  int port = listener.BindListenRange(cfg_->worker_port, cfg_->worker_port + cfg_->nport_trial);
+  utils::Check(port != -1, "cannot listen on a worker port in [%d, %d)", cfg_->worker_port,
                cfg_->worker_port + cfg_->nport_trial);
-  listener.Listen();
 
   auto adopt = [topo](TcpSocket &&sock, int peer) {
     PeerLink *l = topo->Find(peer);

@@ -543,9 +543,8 @@ namespace {
 void LoopbackPair(rabit::net::TcpSocket *a, rabit::net::TcpSocket *b) {
   rabit::net::TcpSocket lis;
   lis.Create();
-  const int port = lis.BindRange(19500, 20500);
+  const int port = lis.BindListenRange(19500, 20500);
   EXPECT(port > 0);
-  lis.Listen();
   a->Create();
   EXPECT(a->Connect("127.0.0.1", port));
   *b = lis.Accept();

@@ -20,7 +20,10 @@ from rabit_amd.launcher import LocalJob  # noqa: E402
 
 WORLD, NITER = 10, 3
 NOPS = 11  # recover_test per iteration at 10 ranks: Max, 4 string broadcasts (2 ops each), Sum, Allgather
-SEEDS = list(range(101, 133))  # 32 seeds
+# 32 committed seeds; XRABIT_CHAOS_SEEDS="a-b" (or "a,b,...") runs others (fuzzing)
+_SPEC = os.environ.get("XRABIT_CHAOS_SEEDS", "")
+SEEDS = (list(range(int(_SPEC.split("-")[0]), int(_SPEC.split("-")[1]) + 1)) if "-" in _SPEC else
+         [int(s) for s in _SPEC.split(",")] if _SPEC else list(range(101, 133)))
 MODES = ["global", "local", "lazy"]
 
 
