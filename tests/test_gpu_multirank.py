@@ -186,12 +186,14 @@ def test_device_chaos(seed):
         pytest.skip("no GPU")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from chaos_points import draw
-    points = draw(seed, 4, 4, 3, wheres=(0, 3, 3, 1))
-    rc, out = _run("device_ft.py", 4, points, attempts=6, timeout=240)
+    world = int(os.environ.get("XRABIT_DEVICE_CHAOS_WORLD", "4"))  # (fuzzing: up to 8)
+    points = draw(seed, world, 4, 3, wheres=(0, 3, 3, 1))
+    rc, out = _run("device_ft.py", world, points, attempts=6, timeout=240)
     if "Too many nodes went down" in out:
         return  # every holder of some data died: the engine says so instead of hanging
     assert rc == 0, "seed %d points %s\n%s" % (seed, points, out[-5000:])
-    assert out.count("DEVFT OK") == 4, "seed %d points %s\n%s" % (seed, points, out[-3000:])
+    assert out.count("DEVFT OK") == world, "seed %d points %s\n%s" % (seed, points,
+                                                                      out[-3000:])
 
 
 def test_recovery_epoch_adopts_calibration():
