@@ -145,11 +145,14 @@ class RabitTracker:
         self.print_fn = print_fn or (lambda msg: print(msg, end="" if msg.endswith("\n") else "\n",
                                                        flush=True))
         self.sock = None
+        # SO_REUSEADDR lets two trackers starting at once both bind a free port; only the first
+        # listen() succeeds, so a listen that fails moves on to the next port as well
         for p in range(port, port_end):
             s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             try:
                 s.bind((host_ip, p))
+                s.listen(256)
             except OSError:
                 s.close()
                 continue
@@ -157,7 +160,6 @@ class RabitTracker:
             break
         if self.sock is None:
             raise OSError("no free tracker port in [%d, %d)" % (port, port_end))
-        self.sock.listen(256)
         self.thread: Optional[threading.Thread] = None
         self.error: Optional[BaseException] = None
         self.start_time = None

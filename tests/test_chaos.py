@@ -18,7 +18,8 @@ from chaos_points import draw  # noqa: E402
 
 from rabit_amd.launcher import LocalJob  # noqa: E402
 
-WORLD, NITER = 10, 3
+WORLD = int(os.environ.get("XRABIT_CHAOS_WORLD", "10"))  # (fuzzing other worlds)
+NITER = 3
 NOPS = 11  # recover_test per iteration at 10 ranks: Max, 4 string broadcasts (2 ops each), Sum, Allgather
 # 32 committed seeds; XRABIT_CHAOS_SEEDS="a-b" (or "a,b,...") runs others (fuzzing)
 _SPEC = os.environ.get("XRABIT_CHAOS_SEEDS", "")
